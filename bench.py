@@ -1,0 +1,176 @@
+"""Throughput of the batched SmartNanogridEnv hot path on MI355X.
+
+Metric (BASELINE.json): env-steps/sec (whole node) at 65,536 envs x 10 chargers, 24-step day.
+One bench "step" = one simulated day for every env on every GPU: GPU-RNG reset (new
+vehicles) + 24 fused step kernels (+ one RCCL all-gather of the per-env day returns when
+N > 1), replayed as one hipGraph.  Actions are synthetic (uniform in the action Box, 20 %
+exact zeros), pre-generated on the device outside the timed region.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--chargers C] [--no-cpu-baseline]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints one JSON line.  `roofline` describes the dominant kernel (the fused step):
+achieved = algorithmic bytes per launch / mean launch time from HIP events captured around
+every step kernel in the graph (the last replay of the timed region); `traffic` comes from
+the committed rocprofv3 PMC summary (profiles/), null if absent.  `cpu_baseline` is the C
+oracle (a scalar port of the reference step/reset) on one host core, bounded sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "smart-nanogrid-gym_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "env-steps/sec (whole node) at N=65,536 envs × 10 chargers, 24-step day"
+
+
+def step_kernel_bytes(n):
+    """Algorithmic bytes one env moves in one fused step (b-pv, no requested-SoC stream):
+    actions 4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N + scenario word 4N
+    + static SoC 8N + BESS r/w 16 + PV ratio 8 + day-return r/w 16 = 40N + 89."""
+    return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 4 * n + 8 * n + 16 + 8 + 16
+
+
+def cpu_baseline(chargers, budget_s):
+    import oracle as O
+    kw = dict(number_of_chargers=chargers, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    cfg = O.OracleConfig(**kw)
+    A = cfg.act_dim
+    batch = 256
+    rng = np.random.default_rng(0)
+    acts = rng.uniform(0, 1, (cfg.T, batch, A)).astype(np.float32)
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    acts[rng.random(acts.shape) < 0.2] = 0
+    envs = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < budget_s:
+        O.run_batch(cfg, batch, envs, 1, acts)
+        envs += batch
+    dt = time.perf_counter() - t0
+    return {"value": envs * cfg.T / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
+            "sample": f"{envs} envs x 1 day (reset + 24 steps each), b-pv N={chargers} sparse 1h, "
+                      f"C oracle (scalar restatement of the reference) on 1 host thread, {dt:.1f} s"}
+
+
+def load_pmc_traffic(n_envs, chargers):
+    """Per-launch HBM bytes of the step kernel from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if d.get("envs") == n_envs and d.get("chargers") == chargers:
+            return d.get("bytes_per_launch")
+    except Exception:
+        return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20, help="timed simulated days")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--chargers", type=int, default=10)
+    ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv
+
+    E, N = args.envs, args.chargers
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
+              battery_system_available_in_model=True)
+    venv = SmartNanogridVecEnv(E, seed=args.seed + rank * E, device=local, rng="device", **kw)
+    T, A = venv.timesteps, venv.act_dim
+    g = torch.Generator(device=device).manual_seed(args.seed + rank)
+    low = torch.tensor(venv.action_space.low, device=device)
+    high = torch.tensor(venv.action_space.high, device=device)
+    acts = low + (high - low) * torch.rand((T, E, A), generator=g, device=device)
+    acts = torch.where(torch.rand(acts.shape, generator=g, device=device) < 0.2, torch.zeros_like(acts), acts)
+    acts = acts.contiguous()
+    # the bench's info: only the per-env day return (for the all-gather), no diagnostics
+    venv._info.flags = None
+    graph = EpisodeGraph(venv, acts, with_reset=True)
+    gathered = torch.empty(world * E, dtype=torch.float64, device=device) if world > 1 else None
+
+    def day():
+        graph.launch()
+        if dist is not None:
+            dist.all_gather_into_tensor(gathered, venv.return_d)
+
+    for _ in range(args.warmup):
+        day()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        day()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = graph.step_kernel_ms()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    # sanity: a day's returns are finite and <= 0
+    ret = venv.return_d.cpu().numpy()
+    assert np.isfinite(ret).all() and (ret <= 0).all()
+
+    if rank == 0:
+        env_steps = world * E * T * args.steps
+        value = env_steps / elapsed
+        launch_s = float(np.mean(kernel_ms)) / 1e3
+        bpl = step_kernel_bytes(N) * E
+        achieved = bpl / launch_s / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N),
+                "kernel": "sng::step_kernel<10>", "bytes_per_launch": bpl,
+                "mean_launch_us": round(launch_s * 1e6, 3)}
+        cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_budget)
+        out = {"metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+               "config": {"workload": f"{E} envs/GPU x {N} chargers x {T}-step day, b-pv bounded sparse 1h, "
+                                      "GPU-RNG reset + 24 fused steps per bench step (hipGraph)",
+                          "envs_per_gpu": E, "chargers": N, "timesteps": T,
+                          "step_unit": "one simulated day of every env",
+                          "parallelism": f"env-sharded x{world}" + (", RCCL all-gather of day returns" if world > 1 else "")},
+               "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(out))
+    graph.close()
+    venv.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,219 @@
+/*
+ * sng.h -- C ABI of the MI355X-native batched SmartNanogridEnv (libsng.so).
+ *
+ * Drop-in boundary for the reference's step()/reset() hot path.  The reference
+ * (Dellintel98/smart-nanogrid-gym, pure Python) has no FFI of its own; its
+ * plugin surface is the gym.Env it registers as 'SmartNanogridEnv-v0'
+ * (smart_nanogrid_gym/__init__.py:4-8).  Each entry point below names the
+ * reference interface it replaces.  The Python mirror of that interface
+ * (smart-nanogrid-gym_amd/smart_nanogrid_gym/) binds these symbols with ctypes;
+ * INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - Plain C types only.  Device buffers are raw device pointers (e.g. a torch
+ *     tensor's data_ptr()); `stream` is an opaque hipStream_t (NULL = default).
+ *   - Every call returns SNG_OK (0) or a negative SngStatus; the message is in
+ *     sng_last_error(env) (or sng_last_error(NULL) for sng_create failures).
+ *   - All calls on one handle must come from one host thread at a time.
+ *   - Layouts at the boundary: actions float32 [num_envs][act_dim] row-major,
+ *     observations float32 [num_envs][obs_dim] row-major, reward float64
+ *     [num_envs], done uint8 [num_envs] -- exactly the per-env arrays the
+ *     reference returns, stacked.
+ */
+#ifndef SNG_H
+#define SNG_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SNG_ABI_VERSION 1
+
+typedef enum SngStatus {
+    SNG_OK = 0,
+    SNG_ERR_INVALID_ARGUMENT = -1,   /* ValueError in the reference */
+    SNG_ERR_UNSUPPORTED = -2,        /* configuration the reference cannot run either */
+    SNG_ERR_HIP = -3,                /* HIP runtime failure */
+    SNG_ERR_STATE = -4,              /* call out of order (e.g. step before reset) */
+    SNG_ERR_OUT_OF_MEMORY = -5
+} SngStatus;
+
+/* vehicle_uncharged_penalty_mode, charging_station.py:50-60 */
+typedef enum SngPenaltyMode {
+    SNG_PENALTY_NONE = 0,            /* 'no_penalty' */
+    SNG_PENALTY_ON_DEPARTURE = 1,    /* 'on_departure' */
+    SNG_PENALTY_SPARSE = 2,          /* 'sparse' */
+    SNG_PENALTY_DENSE = 3            /* 'dense' */
+} SngPenaltyMode;
+
+/* How sng_reset draws the new day's vehicles. */
+typedef enum SngRngMode {
+    /* Host MT19937 streams identical to the reference's global RNGs: environment i
+     * reproduces `np.random.seed(seed + i); random.seed(seed + i)` followed by the
+     * reference's reset()/step() sequence (charging_station.py:200-279,
+     * smart_nanogrid_environment.py:190,358).  Generated on the host CPU threads. */
+    SNG_RNG_REFERENCE = 0,
+    /* Counter-based Philox streams on the GPU: same distributions, different draws.
+     * Fully device-resident; graph-capturable. */
+    SNG_RNG_DEVICE = 1
+} SngRngMode;
+
+/* Per-env flag bits reported by sng_read_errors / SngInfo.flags. */
+#define SNG_FLAG_NEGATIVE_DEMAND  0x1u  /* ValueError, central_management_system.py:158-159 */
+#define SNG_FLAG_CHARGING_MODE    0x2u  /* ValueError, charger.py:88/138, battery_energy_storage_system.py:230/262 */
+#define SNG_FLAG_BESS_SOC_ABOVE_1 0x4u  /* ValueError, penaliser.py:110-111 */
+#define SNG_FLAG_V2X_BREAKPOINT   0x8u  /* breakpoint(), central_management_system.py:160-165 (not an error) */
+
+/* Constructor keyword arguments of SmartNanogridEnv (smart_nanogrid_environment.py:41-43)
+ * plus the module constants the reference hard-codes, with the reference's values as
+ * defaults (sng_config_defaults). */
+typedef struct SngConfig {
+    int32_t abi_version;                     /* = SNG_ABI_VERSION */
+    int32_t number_of_chargers;              /* N (1..128) */
+    double time_interval_hours;              /* set_time_interval(), :134-147 ('1h' -> 1.0) */
+    int32_t price_model;                     /* accountant.py:245-288, 0..4 */
+    int32_t pv_system_available;             /* pv_system_available_in_model */
+    int32_t battery_system_available;        /* battery_system_available_in_model */
+    int32_t vehicle_to_everything;           /* vehicle_to_everything */
+    int32_t different_vehicle_capacities;    /* enable_different_vehicle_battery_capacities */
+    int32_t requested_state_of_charge;       /* enable_requested_state_of_charge */
+    int32_t charging_mode_bounded;           /* charging_mode == 'bounded' */
+    int32_t penalty_mode;                    /* SngPenaltyMode */
+    int32_t numpy_legacy_promotion;          /* 1: NumPy<2 float64 EV power (the recorded KATs) */
+    double grid_cost_weight;                 /* accountant.py:222 -> 0.75 */
+    double battery_penalty_weight;           /* penaliser.py:181 -> 0.8 */
+    double selling_price_coefficient;        /* accountant.py:193 -> 0.8 */
+    /* BESS, central_management_system.py:35 */
+    double bess_capacity_kwh;                /* 80 */
+    double bess_initial_soc;                 /* 0.5 */
+    double bess_max_charging_kw;             /* 44 */
+    double bess_max_discharging_kw;          /* 44 */
+    double bess_charging_efficiency;         /* 0.95 */
+    double bess_discharging_efficiency;      /* 0.95 */
+    double bess_depth_of_discharge;          /* 0.15 */
+    /* EV charger, charger.py:20-23 */
+    double ev_max_power_kw;                  /* 22 */
+    double ev_efficiency;                    /* 0.95 */
+    /* PV input: per-minute irradiance (W/m^2), solar_irradiance.mat['irradiance'] */
+    const double *irradiance_per_minute;
+    int64_t irradiance_minutes;
+} SngConfig;
+
+typedef struct SngDims {
+    int32_t obs_dim;        /* smart_nanogrid_environment.py:99-105 */
+    int32_t act_dim;        /* :110-127 */
+    int32_t timesteps;      /* 24 / dt */
+    int32_t number_of_chargers;
+    int64_t num_envs;
+} SngDims;
+
+/* Optional per-step diagnostics: device pointers, each [num_envs]; NULL = not written.
+ * Names follow the results dict of CentralManagementSystem.manage_nanogrid
+ * (central_management_system.py:128-155). */
+typedef struct SngInfo {
+    double *grid_power;                  /* 'Grid power' */
+    double *total_charging_power;        /* 'Total charging power' */
+    double *total_discharging_power;     /* 'Total discharging power' */
+    double *battery_state_of_charge;     /* 'Battery state of charge' */
+    double *total_vehicle_penalty;       /* 'Total vehicle penalty' */
+    double *total_battery_penalty;       /* 'Total battery penalty' */
+    double *grid_energy_cost;            /* 'Grid energy cost' */
+    double *total_cost;                  /* 'Total cost' */
+    double *utilized_solar_energy;       /* 'Utilized solar energy' */
+    double *battery_power_value;         /* 'Battery power value' */
+    double *battery_calculated_power;    /* 'Battery calculated power value' */
+    double *nonexistent_vehicle_penalty; /* 'DisCharging nonexistent vehicles penalty' */
+    double *initial_battery_soc;         /* 'Initial battery state of charge' */
+    uint32_t *flags;                     /* SNG_FLAG_* raised by this step */
+    double *episode_return;              /* accumulated: += reward (zeroed by every reset) */
+} SngInfo;
+
+/* A scenario in the reference's own layout (ChargingStation after
+ * generate_new_initial_values / load_initial_values, charging_station.py:119-186):
+ * per env and charger, 25-slot arrays plus padded arrival/departure lists (-1 = none). */
+typedef struct SngScenario {
+    int32_t slots;                 /* 25 (charger.py:16-19) */
+    int32_t max_vehicles;          /* padded list length */
+    const double *soc;             /* [num_envs][N][slots]  'SOC' */
+    const double *occupancy;       /* [num_envs][N][slots]  'Charger_occupancy' */
+    const double *capacity;        /* [num_envs][N][slots]  'Vehicle_capacities' */
+    const double *requested_soc;   /* [num_envs][N][slots]  'Requested_SOC' */
+    const int32_t *arrivals;       /* [num_envs][N][max_vehicles]  'Arrivals' */
+    const int32_t *departures;     /* [num_envs][N][max_vehicles]  'Departures' */
+    const double *pv_ratio;        /* [num_envs] random_pv_shift_ratio */
+} SngScenario;
+
+typedef struct SngEnv SngEnv;
+typedef struct SngGraph SngGraph;
+
+int32_t sng_abi_version(void);
+
+/* Fill `cfg` with the reference's defaults (N=8, '1h', b-pv, bounded, sparse). */
+void sng_config_defaults(SngConfig *cfg);
+
+/* SmartNanogridEnv.__init__ (smart_nanogrid_environment.py:41-129) for num_envs
+ * independent environments on HIP device `device`.  Builds the PV/price tables
+ * (pv_system_manager.py:10-91, accountant.py:235-288), allocates device state.
+ * The BESS starts at bess_initial_soc and, as in the reference, is NOT reset by
+ * sng_reset (central_management_system.py:93-94). */
+int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed, SngEnv **out);
+void sng_destroy(SngEnv *env);
+const char *sng_last_error(const SngEnv *env);
+int sng_get_dims(const SngEnv *env, SngDims *out);
+int sng_get_timestep(const SngEnv *env);
+
+/* SmartNanogridEnv.reset() (smart_nanogrid_environment.py:320-360): new day for every
+ * env, timestep 0, writes the t=0 observation into obs[num_envs][obs_dim]. */
+int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream);
+
+/* reset(generate_new_initial_values=False) (:362-366, charging_station.py:119-136):
+ * start a day from a given scenario (host memory, reference layout). */
+int sng_reset_from_scenario(SngEnv *env, const SngScenario *scenario, float *obs, void *stream);
+
+/* SmartNanogridEnv.step(actions) (smart_nanogrid_environment.py:149-197) for every env:
+ * one fused kernel.  reward = -total cost (f64), done = 1 at the end of the day.
+ * `info` may be NULL.  Asynchronous on `stream`. */
+int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
+             const SngInfo *info, void *stream);
+
+/* Sticky per-env error flags (SNG_FLAG_*), copied to host; synchronises. */
+int sng_read_errors(SngEnv *env, uint32_t *host_flags, int clear);
+
+/* State access for resume / parity injection (host arrays of num_envs doubles). */
+int sng_get_battery_soc(SngEnv *env, double *host_soc);
+int sng_set_battery_soc(SngEnv *env, const double *host_soc);
+int sng_get_pv_ratio(SngEnv *env, double *host_ratio);
+/* EV state of charge SOC[c, t] after the last step, host [num_envs][N]. */
+int sng_get_vehicle_soc(SngEnv *env, double *host_soc);
+
+/* Constant tables as built at create (host copies; n = 2*T). */
+int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_power, double *price,
+                   double *price_max, int32_t *n);
+
+/* One full day captured as a hipGraph: [device-RNG reset] + T fused steps.  actions
+ * holds T consecutive [num_envs][act_dim] blocks; obs/reward/done are overwritten every
+ * step; info may be NULL.  Replays draw a new day each time. */
+int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
+                     const SngInfo *info, int with_reset, SngGraph **out);
+int sng_graph_launch(SngGraph *graph, void *stream);
+/* Device time (ms) of each of the T step kernels in the most recent replay, measured by
+ * HIP events captured around every step kernel in the graph.  Synchronises. */
+int sng_graph_step_times(SngGraph *graph, float *ms_per_step, int32_t n);
+void sng_graph_destroy(SngGraph *graph);
+
+/* Host-only entry points (no GPU needed): the reference-RNG scenario generator, for
+ * checking against numpy/Python streams on CPU.  Outputs in SngScenario layout for
+ * `num_envs` envs seeded seed+i; `episode` = number of days already drawn. */
+int sng_host_generate_scenarios(const SngConfig *cfg, int64_t num_envs, uint64_t seed, int32_t episodes,
+                                double *soc, double *occupancy, double *capacity, double *requested_soc,
+                                int32_t *arrivals, int32_t *departures, int32_t max_vehicles,
+                                double *pv_ratio);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SNG_H */

@@ -1,0 +1,926 @@
+// sng_api.cpp -- host side of libsng.so: the C ABI declared in include/sng.h.
+//
+// Owns the per-handle device state, builds the constant tables, turns days in the
+// reference's own layout (25-slot arrays + arrival/departure lists) into the packed
+// per-charger-step words the step kernel reads, generates reference-exact days on host
+// threads (MT19937 streams), and captures whole days into hipGraphs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "sng.h"
+#include "sng_layout.h"
+#include "sng_mt.h"
+
+namespace sng {
+hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
+                       double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream);
+hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
+                           int vec_io, hipStream_t stream);
+hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
+                           hipStream_t stream);
+}  // namespace sng
+
+using namespace sng;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+constexpr int kMaxVehicles = 32;
+
+// numpy pairwise_sum (contiguous float64), used by ndarray.mean() in
+// PVSystemManager.calculate_solar_irradiance_mean (pv_system_manager.py:322-332)
+double pairwise_sum(const double *a, long n) {
+    if (n < 8) {
+        double res = 0.0;
+        for (long i = 0; i < n; ++i) res += a[i];
+        return res;
+    }
+    if (n <= 128) {
+        double r[8];
+        for (int j = 0; j < 8; ++j) r[j] = a[j];
+        long i = 8;
+        for (; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; ++i) res += a[i];
+        return res;
+    }
+    long n2 = n / 2;
+    n2 -= n2 % 8;
+    return pairwise_sum(a, n2) + pairwise_sum(a + n2, n - n2);
+}
+
+struct HostTables {
+    std::vector<double> irr, pv_power, price;
+    double irr_max = 0, price_max = 0;
+};
+
+// PVSystemManager (pv_system_manager.py:10-91) and Accountant price tables (accountant.py:204-288)
+bool build_tables(const SngConfig &c, int T, HostTables &tb, std::string &err) {
+    const double dt = c.time_interval_hours;
+    const int steps_min = (int)(60 * dt);
+    const int padded = 2 * T;
+    if ((int64_t)padded * steps_min > c.irradiance_minutes) {
+        err = "irradiance data too short for two days at this time interval";
+        return false;
+    }
+    tb.irr.assign(padded, 0.0);
+    tb.pv_power.assign(padded, 0.0);
+    for (int k = 0; k < padded; ++k)
+        tb.irr[k] = pairwise_sum(c.irradiance_per_minute + (int64_t)k * steps_min, steps_min) / (double)steps_min;
+    double mx = 0.0;
+    for (double v : tb.irr)
+        if (v >= 0 && v > mx) mx = v;
+    tb.irr_max = mx;
+    const double scaling_pv = ((2.279 * 1.134) * 20) * 0.21 / 1000;   // PVSystem(...), :305, :360-361
+    for (int k = 0; k < padded; ++k) tb.pv_power[k] = ((tb.irr[k] * scaling_pv) * 1.5) / dt;
+
+    const double high = (0.028 + 0.148933333) + 0.014;   // set_grid_tariffs, accountant.py:204-211
+    const double low = (0.013333333 + 0.087613333) + 0.014;
+    static const double m1[24] = {0.05, 0.05, 0.05, 0.05, 0.05, 0.05, 0.05, 0.1, 0.1, 0.1, 0.1, 0.1,
+                                  0.1,  0.1,  0.1,  0.1,  0.1,  0.1,  0.1,  0.1, 0.05, 0.05, 0.05, 0.05};
+    static const double m2[24] = {0.05, 0.05, 0.05, 0.05, 0.05, 0.06, 0.07, 0.08, 0.09, 0.1,  0.1,  0.1,
+                                  0.08, 0.06, 0.05, 0.05, 0.05, 0.06, 0.06, 0.06, 0.06, 0.05, 0.05, 0.05};
+    static const double m3[24] = {0.071, 0.060, 0.056, 0.056, 0.056, 0.060, 0.060, 0.060, 0.066, 0.066, 0.076, 0.080,
+                                  0.080, 0.1,   0.1,   0.076, 0.076, 0.1,   0.082, 0.080, 0.085, 0.079, 0.086, 0.070};
+    static const double m4[24] = {0.1, 0.1, 0.05, 0.05, 0.05, 0.05, 0.05, 0.08, 0.08, 0.1,  0.1,  0.1,
+                                  0.1, 0.1, 0.1,  0.1,  0.1,  0.06, 0.06, 0.06, 0.1,  0.1,  0.1,  0.1};
+    double day[24];
+    switch (c.price_model) {
+        case 0:
+            for (int h = 0; h < 24; ++h) day[h] = (h < 7 || h >= 20) ? low : high;   // :256-260
+            break;
+        case 1: std::memcpy(day, m1, sizeof day); break;
+        case 2: std::memcpy(day, m2, sizeof day); break;
+        case 3: std::memcpy(day, m3, sizeof day); break;
+        case 4: std::memcpy(day, m4, sizeof day); break;
+        default:
+            err = "price_model must be 0..4 (model 5 raises TypeError in accountant.py:277-278)";
+            return false;
+    }
+    tb.price.assign(kPriceLen, 0.0);
+    for (int k = 0; k < kPriceLen; ++k) tb.price[k] = day[k % 24];   // concatenate([day, day]), :287
+    mx = 0.0;
+    for (double v : tb.price)
+        if (v >= 0 && v > mx) mx = v;
+    tb.price_max = mx;
+    return true;
+}
+
+bool in_list(const int32_t *l, int n, int v) {
+    for (int i = 0; i < n; ++i)
+        if (l[i] == v) return true;
+    return false;
+}
+
+int list_len(const int32_t *l, int V) {
+    int n = 0;
+    while (n < V && l[n] >= 0) ++n;
+    return n;
+}
+
+// One day of one environment in the reference's layout.
+struct DayView {
+    double *soc, *occ, *cap, *req;   // [N][25]
+    int32_t *arr, *dep;              // [N][V], -1 padded
+    int V;
+};
+
+// ChargingStation.generate_initial_vehicle_presence_per_charger and the draws it makes
+// (charging_station.py:200-279), clear_initialisation_variables first (:138-150).
+bool generate_day(const SngConfig &c, int T, MT19937 &rng, DayView d) {
+    const int N = c.number_of_chargers;
+    const double dt = c.time_interval_hours;
+    std::fill(d.soc, d.soc + N * kSlots, 0.0);
+    std::fill(d.occ, d.occ + N * kSlots, 0.0);
+    std::fill(d.cap, d.cap + N * kSlots, 0.0);
+    std::fill(d.req, d.req + N * kSlots, 0.0);
+    std::fill(d.arr, d.arr + N * d.V, -1);
+    std::fill(d.dep, d.dep + N * d.V, -1);
+    for (int ch = 0; ch < N; ++ch) {
+        double *soc = d.soc + ch * kSlots, *occ = d.occ + ch * kSlots, *cap = d.cap + ch * kSlots,
+               *req = d.req + ch * kSlots;
+        int32_t *arr = d.arr + ch * d.V, *dep_l = d.dep + ch * d.V;
+        int na = 0;
+        bool present = false, cap_gen = false, req_gen = false;
+        int dep = 0;
+        double cur_cap = 0, cur_req = 0;
+        for (int t = 0; t < T; ++t) {
+            if (!present) {
+                const double r = rng.random();
+                if ((r - 0.1) > 0.5 && t < T) {   // round(random.rand() - 0.1) == 1, :214-215
+                    present = true;
+                    soc[t] = rng.uniform(0.1, 0.9);                              // :257-259
+                    {                                                            // discarded draw, :219
+                        const double lo = soc[t] <= 0.9 ? soc[t] + 0.1 : 1.0;
+                        (void)rng.uniform(lo, 1.0);
+                    }
+                    if (c.different_vehicle_capacities && !cap_gen) {
+                        cur_cap = (double)rng.randint(15, 120);                  // :267-269
+                        cap_gen = true;
+                    } else if (!c.different_vehicle_capacities && !cap_gen) {
+                        cur_cap = 40;
+                        cap_gen = true;
+                    }
+                    if (c.requested_state_of_charge && !req_gen) {
+                        const double lo = soc[t] <= 0.9 ? soc[t] + 0.1 : 1.0;   // :261-265
+                        cur_req = rng.uniform(lo, 1.0);
+                        req_gen = true;
+                    } else if (!c.requested_state_of_charge && !req_gen) {
+                        cur_req = 1.0;
+                        req_gen = true;
+                    }
+                    if (na >= d.V) return false;
+                    arr[na] = t;
+                    // generate_random_vehicle_departure_time, :271-279
+                    const int max_charging = t + (int)(10 / dt);
+                    const int max_departing = T + (int)(1 / dt);
+                    const int high = std::min(max_charging, max_departing);
+                    const int low = t + (int)(4 / dt);
+                    dep = (low >= high) ? low : (int)rng.randint(low, high);
+                    dep_l[na] = dep;
+                    ++na;
+                }
+            }
+            if (present && t < dep) {
+                occ[t] = 1;
+                cap[t] = cur_cap;
+                req[t] = cur_req;
+            } else {
+                present = false;
+                occ[t] = 0;
+                cap[t] = 0;
+                cap_gen = false;
+                cur_cap = 0.0;
+                req[t] = 0;
+                cur_req = 0;
+                req_gen = false;
+            }
+        }
+    }
+    return true;
+}
+
+// Membership test of find_vehicles_for_penalty_check (charging_station.py:42-63, 79-90)
+// for the list built by observe(t).
+bool penalty_window(int mode, const int32_t *deps, int nd, int t) {
+    switch (mode) {
+        case SNG_PENALTY_ON_DEPARTURE: return in_list(deps, nd, t + 1);
+        case SNG_PENALTY_SPARSE:
+            return in_list(deps, nd, t + 1) || in_list(deps, nd, t + 2) || in_list(deps, nd, t + 3);
+        case SNG_PENALTY_DENSE: return true;
+        default: return false;
+    }
+}
+
+// Encode one env's day into the dense per-charger-step timeline (sng_layout.h).
+// req_out may be null; need_req reports whether any penalised requested SoC differs from 1.0.
+bool encode_day(const Params &p, int64_t E, int64_t e, const DayView &d, uint32_t *word, double *aux,
+                double *req_out, double *pen0, bool *need_req, std::string &err) {
+    const int N = p.n, T = p.T;
+    double pen_t0 = 0.0;
+    for (int c = 0; c < N; ++c) {
+        const double *soc = d.soc + c * kSlots, *occ = d.occ + c * kSlots, *cap = d.cap + c * kSlots,
+                     *req = d.req + c * kSlots;
+        const int32_t *arr = d.arr + c * d.V, *dep = d.dep + c * d.V;
+        const int na = list_len(arr, d.V), nd = list_len(dep, d.V);
+        for (int t = 0; t < T; ++t) {
+            const double o = occ[t];
+            if (o != 0.0 && o != 1.0) {
+                err = "occupancy values must be 0 or 1";
+                return false;
+            }
+            const bool occupied = (o == 1.0);
+            const bool arrived = in_list(arr, na, t);
+            const int prev = arrived ? t : (t >= 1 ? t - 1 : kSlots - 1);   // python index t-1
+            // SOC[prev] is the running value only when step t-1 wrote it (charger occupied at t-1)
+            const bool running = !arrived && t >= 1 && occ[t - 1] == 1.0;
+            uint32_t capv = 0, rem = 0;
+            double a = 0.0;
+            if (occupied) {
+                const double cv = cap[prev];
+                if (!(cv >= 0.0 && cv <= 255.0 && cv == std::floor(cv))) {
+                    err = "vehicle capacities must be integers in [0, 255]";
+                    return false;
+                }
+                capv = (uint32_t)cv;
+                if (t == 0 && !arrived) {
+                    err = "charger occupied at t=0 without an arrival at t=0";
+                    return false;
+                }
+                int found = -1;
+                for (int v = 0; v < nd; ++v)
+                    if (t <= dep[v]) {
+                        found = dep[v] - t;
+                        break;
+                    }
+                if (found < 0 || found > 255) {
+                    err = "occupied charger without a departure time >= t (or > 255 steps ahead)";
+                    return false;
+                }
+                rem = (uint32_t)found;
+                a = running ? 0.0 : soc[prev];
+            } else {
+                a = soc[t];
+            }
+            bool pen = false;
+            if (t >= 1 && occ[t - 1] != 0.0) pen = penalty_window(p.penalty_mode, dep, nd, t - 1);
+            const size_t idx = ((size_t)t * N + c) * (size_t)E + (size_t)e;
+            word[idx] = pack_word(occupied, !running, pen, capv, rem);
+            aux[idx] = a;
+            if (pen) {
+                const double rq = req[t - 1];
+                if (rq != 1.0) *need_req = true;
+                if (req_out) req_out[idx] = rq;
+            } else if (req_out) {
+                req_out[idx] = 0.0;
+            }
+        }
+        // penalty at t = 0 reads python index -1 (slot 24) of SOC / Requested_SOC (penaliser.py:59-69)
+        if (occ[0] != 0.0 && penalty_window(p.penalty_mode, dep, nd, 0)) {
+            const double rq = req[kSlots - 1], cur = soc[kSlots - 1];
+            if (cur < rq - 0.05 * rq) {
+                const double x = (rq - cur) * 10;
+                pen_t0 += x * x;
+            }
+        }
+    }
+    *pen0 = pen_t0;
+    return true;
+}
+
+template <class F>
+void parallel_for(int64_t n, F &&f) {
+    unsigned hw = std::thread::hardware_concurrency();
+    int64_t nt = std::max<int64_t>(1, std::min<int64_t>({(int64_t)(hw ? hw : 4), (int64_t)16, (n + 255) / 256}));
+    if (nt == 1) {
+        f(0, n, 0);
+        return;
+    }
+    std::vector<std::thread> th;
+    const int64_t chunk = (n + nt - 1) / nt;
+    for (int64_t k = 0; k < nt; ++k) {
+        const int64_t b = k * chunk, en = std::min(n, b + chunk);
+        if (b >= en) break;
+        th.emplace_back([&, b, en, k] { f(b, en, (int)k); });
+    }
+    for (auto &x : th) x.join();
+}
+
+}  // namespace
+
+struct SngEnv {
+    SngConfig cfg{};
+    Params p{};
+    HostTables tables;
+    std::vector<double> irradiance;   // owned copy
+    int device = 0;
+    int64_t E = 0;
+    uint64_t seed = 0;
+    int t = -1;                       // -1: never reset; T: day finished
+    bool day_finished = false;
+    int i4 = 0, i10 = 0, i1 = 0;
+    DeviceState ds{};
+    Tables *d_tables = nullptr;
+    // host staging (pinned) for days built on the CPU
+    uint32_t *h_word = nullptr;
+    double *h_aux = nullptr, *h_req = nullptr, *h_ratio = nullptr, *h_pen0 = nullptr;
+    hipEvent_t staging_done = nullptr;
+    // reference RNG streams, one numpy + one python MT19937 per env (allocated on first use)
+    std::vector<MT19937> np_rng, py_rng;
+    std::string err;
+
+    size_t timeline() const { return (size_t)p.T * p.n * (size_t)E; }
+};
+
+struct SngGraph {
+    SngEnv *env = nullptr;
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    std::vector<hipEvent_t> ev;   // [2*T]: recorded around every step kernel of the day
+};
+
+namespace {
+
+int fail(SngEnv *env, int code, const std::string &msg) {
+    if (env) env->err = msg; else g_create_error = msg;
+    return code;
+}
+
+int hip_fail(SngEnv *env, hipError_t e, const char *what) {
+    return fail(env, SNG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(env, expr)                                   \
+    do {                                                     \
+        hipError_t _e = (expr);                              \
+        if (_e != hipSuccess) return hip_fail(env, _e, #expr); \
+    } while (0)
+
+bool aligned16(const void *ptr) { return ((uintptr_t)ptr & 15u) == 0; }
+
+InfoPtrs info_ptrs(const SngInfo *i) {
+    InfoPtrs o{};
+    if (!i) return o;
+    o.grid_power = i->grid_power;
+    o.p_charge = i->total_charging_power;
+    o.p_discharge = i->total_discharging_power;
+    o.bess_soc = i->battery_state_of_charge;
+    o.pen_vehicle = i->total_vehicle_penalty;
+    o.pen_battery = i->total_battery_penalty;
+    o.grid_cost = i->grid_energy_cost;
+    o.total_cost = i->total_cost;
+    o.solar = i->utilized_solar_energy;
+    o.bess_power = i->battery_power_value;
+    o.bess_calc_power = i->battery_calculated_power;
+    o.nonexistent = i->nonexistent_vehicle_penalty;
+    o.bess_initial = i->initial_battery_soc;
+    o.flags = i->flags;
+    o.episode_return = i->episode_return;
+    return o;
+}
+
+int ensure_req(SngEnv *env) {
+    if (!env->ds.req) HIP_TRY(env, hipMalloc(&env->ds.req, env->timeline() * sizeof(double)));
+    return SNG_OK;
+}
+
+int ensure_staging(SngEnv *env, bool with_req) {
+    const size_t n = env->timeline();
+    if (!env->h_word) {
+        HIP_TRY(env, hipHostMalloc(&env->h_word, n * sizeof(uint32_t), hipHostMallocDefault));
+        HIP_TRY(env, hipHostMalloc(&env->h_aux, n * sizeof(double), hipHostMallocDefault));
+        HIP_TRY(env, hipHostMalloc(&env->h_ratio, env->E * sizeof(double), hipHostMallocDefault));
+        HIP_TRY(env, hipHostMalloc(&env->h_pen0, env->E * sizeof(double), hipHostMallocDefault));
+        HIP_TRY(env, hipEventCreateWithFlags(&env->staging_done, hipEventDisableTiming));
+    }
+    if (with_req && !env->h_req) HIP_TRY(env, hipHostMalloc(&env->h_req, n * sizeof(double), hipHostMallocDefault));
+    // the previous upload must have drained before the staging buffers are rewritten
+    HIP_TRY(env, hipEventSynchronize(env->staging_done));
+    return SNG_OK;
+}
+
+// Upload the staged day, then the t = 0 observation.
+int upload_and_observe(SngEnv *env, bool need_req, float *obs, hipStream_t st) {
+    const size_t n = env->timeline();
+    HIP_TRY(env, hipMemcpyAsync(env->ds.word, env->h_word, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(env, hipMemcpyAsync(env->ds.aux, env->h_aux, n * sizeof(double), hipMemcpyHostToDevice, st));
+    if (need_req) {
+        int rc = ensure_req(env);
+        if (rc) return rc;
+        HIP_TRY(env, hipMemcpyAsync(env->ds.req, env->h_req, n * sizeof(double), hipMemcpyHostToDevice, st));
+    }
+    HIP_TRY(env, hipMemcpyAsync(env->ds.ratio, env->h_ratio, env->E * sizeof(double), hipMemcpyHostToDevice, st));
+    HIP_TRY(env, hipMemcpyAsync(env->ds.pen0, env->h_pen0, env->E * sizeof(double), hipMemcpyHostToDevice, st));
+    HIP_TRY(env, hipEventRecord(env->staging_done, st));
+    env->p.req_stream = need_req ? 1 : 0;
+    HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st));
+    env->t = 0;
+    env->day_finished = false;
+    return SNG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t sng_abi_version(void) { return SNG_ABI_VERSION; }
+
+void sng_config_defaults(SngConfig *c) {
+    std::memset(c, 0, sizeof *c);
+    c->abi_version = SNG_ABI_VERSION;
+    c->number_of_chargers = 8;                 // smart_nanogrid_environment.py:41
+    c->time_interval_hours = 1.0;              // :147
+    c->price_model = 0;
+    c->pv_system_available = 1;
+    c->battery_system_available = 1;
+    c->vehicle_to_everything = 0;
+    c->different_vehicle_capacities = 1;
+    c->requested_state_of_charge = 0;
+    c->charging_mode_bounded = 1;
+    c->penalty_mode = SNG_PENALTY_SPARSE;
+    c->numpy_legacy_promotion = 0;
+    c->grid_cost_weight = 0.75;                // accountant.py:222
+    c->battery_penalty_weight = 0.8;           // penaliser.py:181
+    c->selling_price_coefficient = 0.8;        // accountant.py:193
+    c->bess_capacity_kwh = 80;                 // central_management_system.py:35
+    c->bess_initial_soc = 0.5;
+    c->bess_max_charging_kw = 44;
+    c->bess_max_discharging_kw = 44;
+    c->bess_charging_efficiency = 0.95;
+    c->bess_discharging_efficiency = 0.95;
+    c->bess_depth_of_discharge = 0.15;
+    c->ev_max_power_kw = 22;                   // charger.py:20-23
+    c->ev_efficiency = 0.95;
+}
+
+const char *sng_last_error(const SngEnv *env) { return env ? env->err.c_str() : g_create_error.c_str(); }
+
+static int validate(const SngConfig *c, int *T_out, std::string &err) {
+    if (!c) { err = "null config"; return SNG_ERR_INVALID_ARGUMENT; }
+    if (c->abi_version != SNG_ABI_VERSION) { err = "SngConfig.abi_version mismatch"; return SNG_ERR_INVALID_ARGUMENT; }
+    if (c->number_of_chargers < 1 || c->number_of_chargers > kMaxChargers) {
+        err = "number_of_chargers must be in [1, 128]";
+        return SNG_ERR_UNSUPPORTED;
+    }
+    const double dt = c->time_interval_hours;
+    if (!(dt > 0)) { err = "Wrong time interval was provided"; return SNG_ERR_INVALID_ARGUMENT; }
+    const double steps = 24.0 / dt;
+    const int T = (int)steps;
+    if ((double)T != steps) {
+        err = "24h / time_interval must be an integer (the reference never ends the day otherwise)";
+        return SNG_ERR_UNSUPPORTED;
+    }
+    if (T > 24) {
+        err = "time intervals below 1h are not runnable in the reference (25-slot arrays, charger.py:16-19)";
+        return SNG_ERR_UNSUPPORTED;
+    }
+    if (T < 4) { err = "time interval too long (fewer than 4 steps per day)"; return SNG_ERR_UNSUPPORTED; }
+    if (c->penalty_mode < 0 || c->penalty_mode > 3) {
+        err = "Error: Wrong vehicle uncharged - penalty mode provided!";
+        return SNG_ERR_INVALID_ARGUMENT;
+    }
+    if (c->price_model < 0 || c->price_model > 4) { err = "price_model must be 0..4"; return SNG_ERR_UNSUPPORTED; }
+    if (!c->irradiance_per_minute || c->irradiance_minutes <= 0) {
+        err = "irradiance_per_minute is required";
+        return SNG_ERR_INVALID_ARGUMENT;
+    }
+    *T_out = T;
+    return SNG_OK;
+}
+
+int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed, SngEnv **out) {
+    if (!out) return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "null out");
+    *out = nullptr;
+    int T = 0;
+    std::string err;
+    int rc = validate(cfg, &T, err);
+    if (rc) return fail(nullptr, rc, err);
+    if (num_envs < 1) return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "num_envs must be >= 1");
+
+    SngEnv *env = new SngEnv();
+    env->cfg = *cfg;
+    env->irradiance.assign(cfg->irradiance_per_minute, cfg->irradiance_per_minute + cfg->irradiance_minutes);
+    env->cfg.irradiance_per_minute = env->irradiance.data();
+    env->device = device;
+    env->E = num_envs;
+    env->seed = seed;
+    if (!build_tables(env->cfg, T, env->tables, err)) {
+        delete env;
+        return fail(nullptr, SNG_ERR_UNSUPPORTED, err);
+    }
+    const SngConfig &c = env->cfg;
+    Params &p = env->p;
+    p.n = c.number_of_chargers;
+    p.T = T;
+    p.pv = c.pv_system_available ? 1 : 0;
+    p.bess = c.battery_system_available ? 1 : 0;
+    p.v2x = c.vehicle_to_everything ? 1 : 0;
+    p.bounded = c.charging_mode_bounded ? 1 : 0;
+    p.legacy = c.numpy_legacy_promotion ? 1 : 0;
+    p.penalty_mode = c.penalty_mode;
+    p.diff_caps = c.different_vehicle_capacities ? 1 : 0;
+    p.req_enabled = c.requested_state_of_charge ? 1 : 0;
+    p.req_stream = p.req_enabled;
+    p.obs_dim = (1 + p.pv) * 4 + 2 * p.n + p.bess;   // smart_nanogrid_environment.py:99-105
+    p.act_dim = p.n + p.bess;                          // :110-127
+    p.dt = c.time_interval_hours;
+    p.dt_f = (float)c.time_interval_hours;
+    p.ev_power = c.ev_max_power_kw;
+    p.ev_eff = c.ev_efficiency;
+    p.ev_power_f = (float)c.ev_max_power_kw;
+    p.ev_eff_f = (float)c.ev_efficiency;
+    p.bess_cap = c.bess_capacity_kwh;
+    p.bess_pmax_ch = c.bess_max_charging_kw;
+    p.bess_pmax_dis = c.bess_max_discharging_kw;
+    p.bess_eff_ch = c.bess_charging_efficiency;
+    p.bess_eff_dis = c.bess_discharging_efficiency;
+    p.bess_dod = c.bess_depth_of_discharge;
+    p.grid_w = c.grid_cost_weight;
+    p.bat_pen_w = c.battery_penalty_weight;
+    p.sell_coef = c.selling_price_coefficient;
+    env->i4 = (int)(4 / p.dt);
+    env->i10 = (int)(10 / p.dt);
+    env->i1 = (int)(1 / p.dt);
+
+    // host copy of the device tables
+    Tables ht;
+    std::memset(&ht, 0, sizeof ht);
+    const int n_irr = (int)env->tables.irr.size();
+    ht.n_irr = n_irr;
+    for (int k = 0; k < n_irr; ++k) {
+        ht.irr_norm[k] = env->tables.irr[k] / env->tables.irr_max;   // pv_system_manager.py:369-373
+        ht.pv_power[k] = env->tables.pv_power[k];
+    }
+    for (int k = 0; k < kPriceLen; ++k) {
+        ht.price[k] = env->tables.price[k];
+        ht.price_norm[k] = env->tables.price[k] / env->tables.price_max;   // accountant.py:229-233
+    }
+
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) {
+        delete env;
+        return fail(nullptr, SNG_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    }
+    auto alloc = [&](void **ptr, size_t bytes) -> bool {
+        hipError_t r = hipMalloc(ptr, bytes);
+        if (r != hipSuccess) {
+            g_create_error = std::string("hipMalloc: ") + hipGetErrorString(r);
+            return false;
+        }
+        return true;
+    };
+    const size_t E = (size_t)num_envs, tl = env->timeline();
+    DeviceState &ds = env->ds;
+    bool ok = alloc((void **)&ds.soc, E * p.n * sizeof(double)) && alloc((void **)&ds.bess, E * sizeof(double)) &&
+              alloc((void **)&ds.bess0, E * sizeof(double)) && alloc((void **)&ds.ratio, E * sizeof(double)) &&
+              alloc((void **)&ds.pen0, E * sizeof(double)) && alloc((void **)&ds.word, tl * sizeof(uint32_t)) &&
+              alloc((void **)&ds.aux, tl * sizeof(double)) && alloc((void **)&ds.flags, E * sizeof(uint32_t)) &&
+              alloc((void **)&ds.episode, sizeof(uint64_t)) && alloc((void **)&env->d_tables, sizeof(Tables));
+    if (ok && p.req_enabled) ok = alloc((void **)&ds.req, tl * sizeof(double));
+    if (!ok) {
+        std::string msg = g_create_error;
+        sng_destroy(env);
+        return fail(nullptr, SNG_ERR_OUT_OF_MEMORY, msg);
+    }
+    ds.tables = env->d_tables;
+    std::vector<double> b(E, c.bess_initial_soc);
+    std::vector<double> ones(E, 1.0);
+    bool ok2 = hipMemcpy(env->d_tables, &ht, sizeof ht, hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemcpy(ds.bess, b.data(), E * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemcpy(ds.bess0, b.data(), E * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemcpy(ds.ratio, ones.data(), E * sizeof(double), hipMemcpyHostToDevice) == hipSuccess &&
+               hipMemset(ds.pen0, 0, E * sizeof(double)) == hipSuccess &&
+               hipMemset(ds.soc, 0, E * p.n * sizeof(double)) == hipSuccess &&
+               hipMemset(ds.flags, 0, E * sizeof(uint32_t)) == hipSuccess &&
+               hipMemset(ds.episode, 0, sizeof(uint64_t)) == hipSuccess &&
+               hipMemset(ds.word, 0, tl * sizeof(uint32_t)) == hipSuccess &&
+               hipMemset(ds.aux, 0, tl * sizeof(double)) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    if (!ok2) {
+        sng_destroy(env);
+        return fail(nullptr, SNG_ERR_HIP, "device initialisation failed");
+    }
+    *out = env;
+    return SNG_OK;
+}
+
+void sng_destroy(SngEnv *env) {
+    if (!env) return;
+    (void)hipSetDevice(env->device);
+    DeviceState &ds = env->ds;
+    void *dev[] = {ds.soc, ds.bess, ds.bess0, ds.ratio, ds.pen0, ds.word, ds.aux, ds.req, ds.flags, ds.episode,
+                   env->d_tables};
+    for (void *x : dev)
+        if (x) (void)hipFree(x);
+    void *host[] = {env->h_word, env->h_aux, env->h_req, env->h_ratio, env->h_pen0};
+    for (void *x : host)
+        if (x) (void)hipHostFree(x);
+    if (env->staging_done) (void)hipEventDestroy(env->staging_done);
+    delete env;
+}
+
+int sng_get_dims(const SngEnv *env, SngDims *out) {
+    if (!env || !out) return SNG_ERR_INVALID_ARGUMENT;
+    out->obs_dim = env->p.obs_dim;
+    out->act_dim = env->p.act_dim;
+    out->timesteps = env->p.T;
+    out->number_of_chargers = env->p.n;
+    out->num_envs = env->E;
+    return SNG_OK;
+}
+
+int sng_get_timestep(const SngEnv *env) { return env ? env->t : -1; }
+
+int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
+    if (!env || !obs) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(env, hipSetDevice(env->device));
+    hipStream_t st = (hipStream_t)stream;
+    if (rng_mode == SNG_RNG_DEVICE) {
+        if (env->i4 < 2) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
+        env->p.req_stream = env->p.req_enabled;
+        if (env->p.req_stream) {
+            int rc = ensure_req(env);
+            if (rc) return rc;
+        }
+        HIP_TRY(env, launch_generate(env->p, env->ds, env->seed, env->E, env->i4, env->i10, env->i1, st));
+        HIP_TRY(env, launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st));
+        env->t = 0;
+        env->day_finished = false;
+        return SNG_OK;
+    }
+    if (rng_mode != SNG_RNG_REFERENCE) return fail(env, SNG_ERR_INVALID_ARGUMENT, "unknown rng_mode");
+
+    const int N = env->p.n, T = env->p.T;
+    const bool first = env->np_rng.empty();
+    if (first) {
+        env->np_rng.resize(env->E);
+        env->py_rng.resize(env->E);
+        for (int64_t i = 0; i < env->E; ++i) {
+            env->np_rng[i].seed_numpy((uint32_t)(env->seed + (uint64_t)i));
+            env->py_rng[i].seed_python(env->seed + (uint64_t)i);
+        }
+    }
+    const bool with_req = env->p.req_enabled != 0;
+    int rc = ensure_staging(env, with_req);
+    if (rc) return rc;
+    const bool end_draw = env->day_finished;
+    std::vector<std::string> errs(16);
+    std::vector<char> bad(16, 0);
+    parallel_for(env->E, [&](int64_t b, int64_t en, int k) {
+        const int V = kMaxVehicles;
+        std::vector<double> soc(N * kSlots), occ(N * kSlots), cap(N * kSlots), req(N * kSlots);
+        std::vector<int32_t> arr(N * V), dep(N * V);
+        DayView d{soc.data(), occ.data(), cap.data(), req.data(), arr.data(), dep.data(), V};
+        bool need = false;
+        for (int64_t i = b; i < en; ++i) {
+            // the day-end draw of the previous step (smart_nanogrid_environment.py:190)
+            if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
+            if (!generate_day(env->cfg, T, env->np_rng[i], d)) {
+                bad[k] = 1;
+                errs[k] = "more vehicles per charger than supported";
+                return;
+            }
+            env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;   // :358
+            std::string e;
+            if (!encode_day(env->p, env->E, i, d, env->h_word, env->h_aux, with_req ? env->h_req : nullptr,
+                            &env->h_pen0[i], &need, e)) {
+                bad[k] = 1;
+                errs[k] = e;
+                return;
+            }
+        }
+    });
+    for (int k = 0; k < 16; ++k)
+        if (bad[k]) return fail(env, SNG_ERR_INVALID_ARGUMENT, errs[k]);
+    return upload_and_observe(env, with_req, obs, st);
+}
+
+int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void *stream) {
+    if (!env || !sc || !obs) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    if (sc->slots != kSlots) return fail(env, SNG_ERR_INVALID_ARGUMENT, "scenario slots must be 25");
+    if (!sc->soc || !sc->occupancy || !sc->capacity || !sc->requested_soc || !sc->arrivals || !sc->departures ||
+        !sc->pv_ratio || sc->max_vehicles < 1)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "incomplete scenario");
+    HIP_TRY(env, hipSetDevice(env->device));
+    int rc = ensure_staging(env, true);
+    if (rc) return rc;
+    const int N = env->p.n, V = sc->max_vehicles;
+    std::vector<std::string> errs(16);
+    std::vector<char> bad(16, 0), need(16, 0);
+    parallel_for(env->E, [&](int64_t b, int64_t en, int k) {
+        bool nr = false;
+        for (int64_t i = b; i < en; ++i) {
+            const size_t o = (size_t)i * N * kSlots, ol = (size_t)i * N * V;
+            DayView d{const_cast<double *>(sc->soc + o), const_cast<double *>(sc->occupancy + o),
+                      const_cast<double *>(sc->capacity + o), const_cast<double *>(sc->requested_soc + o),
+                      const_cast<int32_t *>(sc->arrivals + ol), const_cast<int32_t *>(sc->departures + ol), V};
+            std::string e;
+            if (!encode_day(env->p, env->E, i, d, env->h_word, env->h_aux, env->h_req, &env->h_pen0[i], &nr, e)) {
+                bad[k] = 1;
+                errs[k] = "env " + std::to_string(i) + ": " + e;
+                return;
+            }
+            env->h_ratio[i] = sc->pv_ratio[i];
+        }
+        need[k] = nr;
+    });
+    bool need_req = env->p.req_enabled != 0;
+    for (int k = 0; k < 16; ++k) {
+        if (bad[k]) return fail(env, SNG_ERR_INVALID_ARGUMENT, errs[k]);
+        need_req = need_req || need[k];
+    }
+    return upload_and_observe(env, need_req, obs, (hipStream_t)stream);
+}
+
+int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done, const SngInfo *info,
+             void *stream) {
+    if (!env || !actions || !obs || !reward || !done) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    if (env->t < 0) return fail(env, SNG_ERR_STATE, "step() before reset()");
+    if (env->t >= env->p.T) return fail(env, SNG_ERR_STATE, "the day is over: call reset()");
+    HIP_TRY(env, hipSetDevice(env->device));
+    const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
+    HIP_TRY(env, launch_step(env->p, env->ds, info_ptrs(info), actions, obs, reward, done, env->E, env->t, vec,
+                             (hipStream_t)stream));
+    env->t += 1;
+    if (env->t == env->p.T) env->day_finished = true;
+    return SNG_OK;
+}
+
+int sng_read_errors(SngEnv *env, uint32_t *host_flags, int clear) {
+    if (!env || !host_flags) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(env, hipSetDevice(env->device));
+    HIP_TRY(env, hipDeviceSynchronize());
+    HIP_TRY(env, hipMemcpy(host_flags, env->ds.flags, env->E * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (clear) HIP_TRY(env, hipMemset(env->ds.flags, 0, env->E * sizeof(uint32_t)));
+    return SNG_OK;
+}
+
+int sng_get_battery_soc(SngEnv *env, double *h) {
+    if (!env || !h) return SNG_ERR_INVALID_ARGUMENT;
+    HIP_TRY(env, hipSetDevice(env->device));
+    HIP_TRY(env, hipDeviceSynchronize());
+    HIP_TRY(env, hipMemcpy(h, env->ds.bess, env->E * sizeof(double), hipMemcpyDeviceToHost));
+    return SNG_OK;
+}
+
+int sng_set_battery_soc(SngEnv *env, const double *h) {
+    if (!env || !h) return SNG_ERR_INVALID_ARGUMENT;
+    HIP_TRY(env, hipSetDevice(env->device));
+    HIP_TRY(env, hipDeviceSynchronize());
+    HIP_TRY(env, hipMemcpy(env->ds.bess, h, env->E * sizeof(double), hipMemcpyHostToDevice));
+    return SNG_OK;
+}
+
+int sng_get_pv_ratio(SngEnv *env, double *h) {
+    if (!env || !h) return SNG_ERR_INVALID_ARGUMENT;
+    HIP_TRY(env, hipSetDevice(env->device));
+    HIP_TRY(env, hipDeviceSynchronize());
+    HIP_TRY(env, hipMemcpy(h, env->ds.ratio, env->E * sizeof(double), hipMemcpyDeviceToHost));
+    return SNG_OK;
+}
+
+int sng_get_vehicle_soc(SngEnv *env, double *h) {
+    if (!env || !h) return SNG_ERR_INVALID_ARGUMENT;
+    HIP_TRY(env, hipSetDevice(env->device));
+    HIP_TRY(env, hipDeviceSynchronize());
+    const int N = env->p.n;
+    std::vector<double> tmp((size_t)N * env->E);
+    HIP_TRY(env, hipMemcpy(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost));
+    for (int64_t e = 0; e < env->E; ++e)
+        for (int c = 0; c < N; ++c) h[e * N + c] = tmp[(size_t)c * env->E + e];
+    return SNG_OK;
+}
+
+int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_power, double *price,
+                   double *price_max, int32_t *n) {
+    if (!env) return SNG_ERR_INVALID_ARGUMENT;
+    const auto &tb = env->tables;
+    if (irr) std::memcpy(irr, tb.irr.data(), tb.irr.size() * sizeof(double));
+    if (pv_power) std::memcpy(pv_power, tb.pv_power.data(), tb.pv_power.size() * sizeof(double));
+    if (price) std::memcpy(price, tb.price.data(), tb.price.size() * sizeof(double));
+    if (irr_max) *irr_max = tb.irr_max;
+    if (price_max) *price_max = tb.price_max;
+    if (n) *n = (int32_t)tb.irr.size();
+    return SNG_OK;
+}
+
+int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
+                     const SngInfo *info, int with_reset, SngGraph **out) {
+    if (!env || !actions || !obs || !reward || !done || !out) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    if (with_reset && env->i4 < 2) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
+    HIP_TRY(env, hipSetDevice(env->device));
+    if (env->p.req_enabled) {
+        int rc = ensure_req(env);
+        if (rc) return rc;
+    }
+    hipStream_t cs;
+    HIP_TRY(env, hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    SngGraph *g = new SngGraph();
+    g->env = env;
+    Params p = env->p;
+    if (with_reset) p.req_stream = p.req_enabled;
+    const InfoPtrs ip = info_ptrs(info);
+    const int64_t E = env->E;
+    const int A = p.act_dim;
+    const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
+    if (e == hipSuccess && with_reset) {
+        e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, cs);
+        if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, cs);
+    }
+    g->ev.assign(2 * (size_t)p.T, nullptr);
+    for (auto &x : g->ev)
+        if (e == hipSuccess) e = hipEventCreate(&x);
+    for (int t = 0; e == hipSuccess && t < p.T; ++t) {
+        e = hipEventRecord(g->ev[2 * t], cs);
+        if (e == hipSuccess)
+            e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
+        if (e == hipSuccess) e = hipEventRecord(g->ev[2 * t + 1], cs);
+    }
+    hipGraph_t graph = nullptr;
+    hipError_t e2 = hipStreamEndCapture(cs, &graph);
+    if (e == hipSuccess) e = e2;
+    if (e == hipSuccess) e = hipGraphInstantiate(&g->exec, graph, nullptr, nullptr, 0);
+    (void)hipStreamDestroy(cs);
+    if (e != hipSuccess) {
+        if (graph) (void)hipGraphDestroy(graph);
+        for (auto x : g->ev)
+            if (x) (void)hipEventDestroy(x);
+        delete g;
+        return hip_fail(env, e, "graph capture");
+    }
+    g->graph = graph;
+    *out = g;
+    return SNG_OK;
+}
+
+int sng_graph_launch(SngGraph *g, void *stream) {
+    if (!g) return SNG_ERR_INVALID_ARGUMENT;
+    SngEnv *env = g->env;
+    HIP_TRY(env, hipSetDevice(env->device));
+    HIP_TRY(env, hipGraphLaunch(g->exec, (hipStream_t)stream));
+    env->t = env->p.T;
+    env->day_finished = true;
+    return SNG_OK;
+}
+
+void sng_graph_destroy(SngGraph *g) {
+    if (!g) return;
+    (void)hipSetDevice(g->env->device);
+    if (g->exec) (void)hipGraphExecDestroy(g->exec);
+    if (g->graph) (void)hipGraphDestroy(g->graph);
+    for (auto x : g->ev)
+        if (x) (void)hipEventDestroy(x);
+    delete g;
+}
+
+int sng_graph_step_times(SngGraph *g, float *ms, int32_t n) {
+    if (!g || !ms) return SNG_ERR_INVALID_ARGUMENT;
+    SngEnv *env = g->env;
+    HIP_TRY(env, hipSetDevice(env->device));
+    const int T = (int)(g->ev.size() / 2);
+    for (int t = 0; t < T && t < n; ++t) {
+        HIP_TRY(env, hipEventSynchronize(g->ev[2 * t + 1]));
+        HIP_TRY(env, hipEventElapsedTime(&ms[t], g->ev[2 * t], g->ev[2 * t + 1]));
+    }
+    return SNG_OK;
+}
+
+int sng_host_generate_scenarios(const SngConfig *cfg, int64_t num_envs, uint64_t seed, int32_t episodes, double *soc,
+                                double *occupancy, double *capacity, double *requested_soc, int32_t *arrivals,
+                                int32_t *departures, int32_t max_vehicles, double *pv_ratio) {
+    int T = 0;
+    std::string err;
+    int rc = validate(cfg, &T, err);
+    if (rc) return fail(nullptr, rc, err);
+    if (num_envs < 1 || episodes < 1 || max_vehicles < 1)
+        return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "bad sizes");
+    const int N = cfg->number_of_chargers;
+    bool overflow = false;
+    for (int64_t i = 0; i < num_envs; ++i) {
+        MT19937 np_rng, py_rng;
+        np_rng.seed_numpy((uint32_t)(seed + (uint64_t)i));
+        py_rng.seed_python(seed + (uint64_t)i);
+        for (int ep = 0; ep < episodes; ++ep) {
+            if (ep > 0) (void)py_rng.py_randint(0, 180);   // day-end draw, smart_nanogrid_environment.py:190
+            const size_t k = (size_t)ep * num_envs + i;
+            DayView d{soc + k * N * kSlots, occupancy + k * N * kSlots, capacity + k * N * kSlots,
+                      requested_soc + k * N * kSlots, arrivals + k * N * max_vehicles,
+                      departures + k * N * max_vehicles, max_vehicles};
+            if (!generate_day(*cfg, T, np_rng, d)) overflow = true;
+            pv_ratio[k] = (double)py_rng.py_randint(0, 180) / 100;
+        }
+    }
+    if (overflow) return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "max_vehicles too small");
+    return SNG_OK;
+}
+
+}  // extern "C"

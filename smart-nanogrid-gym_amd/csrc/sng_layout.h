@@ -1,0 +1,93 @@
+// sng_layout.h -- HBM layout shared by the host code and the HIP kernels.
+//
+// State of arrays, env index fastest everywhere so a wavefront's 64 lanes (64 envs)
+// touch one contiguous 256 B / 512 B run per charger:
+//
+//   soc    f64 [N][E]       SOC[c, t] of the last stepped timestep (charger.py:16 array, one slot)
+//   bess   f64 [E]          BESS state of charge (persists across days)
+//   bess0  f64 [E]          'Initial battery state of charge' of the current day
+//   ratio  f64 [E]          random_pv_shift_ratio of the current day
+//   pen0   f64 [E]          vehicle penalty at t=0 (reads the python index -1 slot; 0 for generated days)
+//   word   u32 [T][N][E]    per charger-step scenario word (bits below)
+//   aux    f64 [T][N][E]    per charger-step static SoC: the "previous" SoC when the word's
+//                           STATIC bit is set (arrival: SOC[c, t] as generated), else the
+//                           SOC[c, t] an unoccupied charger shows
+//   req    f64 [T][N][E]    requested SoC of the vehicle at t-1 (penalty), only when enabled
+//   flags  u32 [E]          sticky SNG_FLAG_* bits
+//
+// word bits (one u32 per charger and timestep):
+//   bit 0      OCC     charger.occupancy[t] == 1
+//   bit 1      STATIC  previous SoC comes from aux (t in vehicle_arrivals, or the slot before
+//                      was not written this day) instead of the running SoC
+//   bit 2      PEN     charger is in the penalty-check list that observe(t-1) built
+//                      (charging_station.py:42-63); evaluated at step t
+//   bits 8-15  CAP     vehicle capacity in kWh used at step t (integer, 15..119 or 40)
+//   bits 16-23 DEP     departure time - t of the vehicle present at t (observation), 0 if none
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define SNG_HD __host__ __device__
+#else
+#define SNG_HD
+#endif
+
+namespace sng {
+
+constexpr uint32_t W_OCC = 1u;
+constexpr uint32_t W_STATIC = 2u;
+constexpr uint32_t W_PEN = 4u;
+constexpr int W_CAP_SHIFT = 8;
+constexpr int W_DEP_SHIFT = 16;
+
+constexpr int kMaxChargers = 128;   // numpy pairwise sum restated for n <= 128 (single level)
+constexpr int kSlots = 25;          // charger.py:16-19
+constexpr int kMaxT = 128;
+constexpr int kPriceLen = 48;       // accountant.py:201, 236
+
+SNG_HD inline uint32_t pack_word(bool occ, bool stat, bool pen, uint32_t cap, uint32_t dep) {
+    return (occ ? W_OCC : 0u) | (stat ? W_STATIC : 0u) | (pen ? W_PEN : 0u) | ((cap & 0xffu) << W_CAP_SHIFT) |
+           ((dep & 0xffu) << W_DEP_SHIFT);
+}
+
+// Constant tables, in device memory, read with scalar (wave-uniform) loads.
+struct Tables {
+    double irr_norm[4 * kMaxT];    // irr[k] / irr_max          (pv_system_manager.py:369-373)
+    double pv_power[4 * kMaxT];    // available_solar_power[k]  (:375-379)
+    double price[kPriceLen];       // energy_price[0, k]        (accountant.py:225-227)
+    double price_norm[kPriceLen];  // energy_price / max        (:229-233)
+    int32_t n_irr;
+};
+
+// Physical constants and switches, passed by value to every kernel.
+struct Params {
+    int32_t n;                // chargers
+    int32_t T;                // steps per day
+    int32_t obs_dim, act_dim;
+    int32_t pv, bess, v2x, bounded, legacy, req_stream, penalty_mode;
+    int32_t diff_caps, req_enabled;
+    double dt;
+    float dt_f;               // float32(dt) for the NEP 50 float32 product
+    float ev_power_f, ev_eff_f;
+    double ev_power, ev_eff;
+    double bess_cap, bess_pmax_ch, bess_pmax_dis, bess_eff_ch, bess_eff_dis, bess_dod;
+    double grid_w, bat_pen_w, sell_coef;
+};
+
+struct DeviceState {
+    double *soc, *bess, *bess0, *ratio, *pen0;
+    uint32_t *word;
+    double *aux, *req;
+    uint32_t *flags;
+    uint64_t *episode;        // device-side day counter for the Philox generator
+    const Tables *tables;
+};
+
+struct InfoPtrs {
+    double *grid_power, *p_charge, *p_discharge, *bess_soc, *pen_vehicle, *pen_battery, *grid_cost, *total_cost,
+        *solar, *bess_power, *bess_calc_power, *nonexistent, *bess_initial;
+    uint32_t *flags;
+    double *episode_return;
+};
+
+}  // namespace sng

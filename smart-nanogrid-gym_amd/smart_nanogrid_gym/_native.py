@@ -1,0 +1,160 @@
+"""ctypes binding of libsng.so (the C ABI in include/sng.h).
+
+The shared library is the only compute path: there is no Python/NumPy fallback, and
+loading fails loudly if the library is missing.  torch is imported first (when present)
+so that libsng.so binds to the HIP runtime torch already loaded (both carry the SONAME
+libamdhip64.so.7) and torch streams / device pointers are valid in both.
+"""
+import ctypes
+import os
+
+try:  # share torch's HIP runtime; torch is the device-memory/stream plumbing
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is part of the image
+    torch = None
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("SNG_LIBRARY", os.path.join(os.path.dirname(PKG_DIR), "lib", "libsng.so"))
+DATA_DIR = os.path.join(PKG_DIR, "data")
+IRRADIANCE_FILE = os.path.join(DATA_DIR, "solar_irradiance_1min.f64")
+
+ABI_VERSION = 1
+SNG_OK = 0
+RNG_REFERENCE = 0
+RNG_DEVICE = 1
+FLAG_NEGATIVE_DEMAND = 0x1
+FLAG_CHARGING_MODE = 0x2
+FLAG_BESS_SOC_ABOVE_1 = 0x4
+FLAG_V2X_BREAKPOINT = 0x8
+
+c_double_p = ctypes.POINTER(ctypes.c_double)
+c_float_p = ctypes.POINTER(ctypes.c_float)
+c_int32_p = ctypes.POINTER(ctypes.c_int32)
+c_uint32_p = ctypes.POINTER(ctypes.c_uint32)
+
+
+class SngConfig(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("number_of_chargers", ctypes.c_int32),
+        ("time_interval_hours", ctypes.c_double),
+        ("price_model", ctypes.c_int32),
+        ("pv_system_available", ctypes.c_int32),
+        ("battery_system_available", ctypes.c_int32),
+        ("vehicle_to_everything", ctypes.c_int32),
+        ("different_vehicle_capacities", ctypes.c_int32),
+        ("requested_state_of_charge", ctypes.c_int32),
+        ("charging_mode_bounded", ctypes.c_int32),
+        ("penalty_mode", ctypes.c_int32),
+        ("numpy_legacy_promotion", ctypes.c_int32),
+        ("grid_cost_weight", ctypes.c_double),
+        ("battery_penalty_weight", ctypes.c_double),
+        ("selling_price_coefficient", ctypes.c_double),
+        ("bess_capacity_kwh", ctypes.c_double),
+        ("bess_initial_soc", ctypes.c_double),
+        ("bess_max_charging_kw", ctypes.c_double),
+        ("bess_max_discharging_kw", ctypes.c_double),
+        ("bess_charging_efficiency", ctypes.c_double),
+        ("bess_discharging_efficiency", ctypes.c_double),
+        ("bess_depth_of_discharge", ctypes.c_double),
+        ("ev_max_power_kw", ctypes.c_double),
+        ("ev_efficiency", ctypes.c_double),
+        ("irradiance_per_minute", c_double_p),
+        ("irradiance_minutes", ctypes.c_int64),
+    ]
+
+
+class SngDims(ctypes.Structure):
+    _fields_ = [("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32), ("timesteps", ctypes.c_int32),
+                ("number_of_chargers", ctypes.c_int32), ("num_envs", ctypes.c_int64)]
+
+
+INFO_FIELDS = ["grid_power", "total_charging_power", "total_discharging_power", "battery_state_of_charge",
+               "total_vehicle_penalty", "total_battery_penalty", "grid_energy_cost", "total_cost",
+               "utilized_solar_energy", "battery_power_value", "battery_calculated_power",
+               "nonexistent_vehicle_penalty", "initial_battery_soc"]
+
+
+class SngInfo(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_void_p) for f in INFO_FIELDS] + [("flags", ctypes.c_void_p),
+                                                               ("episode_return", ctypes.c_void_p)]
+
+
+class SngScenario(ctypes.Structure):
+    _fields_ = [("slots", ctypes.c_int32), ("max_vehicles", ctypes.c_int32),
+                ("soc", c_double_p), ("occupancy", c_double_p), ("capacity", c_double_p),
+                ("requested_soc", c_double_p), ("arrivals", c_int32_p), ("departures", c_int32_p),
+                ("pv_ratio", c_double_p)]
+
+
+EXPORTS = {
+    "sng_abi_version": (ctypes.c_int32, []),
+    "sng_config_defaults": (None, [ctypes.POINTER(SngConfig)]),
+    "sng_create": (ctypes.c_int, [ctypes.POINTER(SngConfig), ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
+                                  ctypes.POINTER(ctypes.c_void_p)]),
+    "sng_destroy": (None, [ctypes.c_void_p]),
+    "sng_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
+    "sng_get_dims": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SngDims)]),
+    "sng_get_timestep": (ctypes.c_int, [ctypes.c_void_p]),
+    "sng_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "sng_reset_from_scenario": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SngScenario), ctypes.c_void_p,
+                                               ctypes.c_void_p]),
+    "sng_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.POINTER(SngInfo), ctypes.c_void_p]),
+    "sng_read_errors": (ctypes.c_int, [ctypes.c_void_p, c_uint32_p, ctypes.c_int]),
+    "sng_get_battery_soc": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "sng_set_battery_soc": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "sng_get_pv_ratio": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "sng_get_vehicle_soc": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "sng_get_tables": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
+                                      c_int32_p]),
+    "sng_graph_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.POINTER(SngInfo), ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_void_p)]),
+    "sng_graph_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "sng_graph_destroy": (None, [ctypes.c_void_p]),
+    "sng_graph_step_times": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int32]),
+    "sng_host_generate_scenarios": (ctypes.c_int, [ctypes.POINTER(SngConfig), ctypes.c_int64, ctypes.c_uint64,
+                                                   ctypes.c_int32, c_double_p, c_double_p, c_double_p, c_double_p,
+                                                   c_int32_p, c_int32_p, ctypes.c_int32, c_double_p]),
+}
+
+_lib = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libsng.so (raises NativeLibraryMissing when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or `make -C smart-nanogrid-gym_amd/csrc` (there is no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        if L.sng_abi_version() != ABI_VERSION:
+            raise NativeLibraryMissing("libsng.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def check(rc, handle=None):
+    if rc != SNG_OK:
+        msg = lib().sng_last_error(handle)
+        raise NativeError(f"libsng error {rc}: {msg.decode() if msg else ''}")
+
+
+def load_irradiance():
+    import numpy as np
+    return np.fromfile(IRRADIANCE_FILE, dtype="<f8")

@@ -1,0 +1,89 @@
+"""SmartNanogridEnv: the single-environment gym surface of the reference
+(smart_nanogrid_gym/envs/smart_nanogrid_environment.py), backed by the batched GPU
+implementation with num_envs = 1.
+
+Same constructor keywords, same spaces, reset() -> (obs, {}), step(a) ->
+(obs float32[obs_dim], reward float64, terminated, False, {}).
+"""
+import numpy as np
+import torch
+
+from .vec_env import SmartNanogridVecEnv
+
+try:  # subclass gym(nasium).Env when available so wrappers / checkers accept it
+    import gymnasium as _gym   # pragma: no cover - not in the image
+except Exception:
+    try:
+        import gym as _gym     # pragma: no cover
+    except Exception:
+        _gym = None
+
+_Base = _gym.Env if _gym is not None else object
+
+
+class SmartNanogridEnv(_Base):
+    metadata = {"render_modes": []}
+
+    def __init__(self, price_model=0, number_of_chargers=8, pv_system_available_in_model=True,
+                 battery_system_available_in_model=True, vehicle_to_everything=False,
+                 enable_different_vehicle_battery_capacities=True, enable_requested_state_of_charge=False,
+                 algorithm_used="", environment_mode="", time_interval="", charging_mode="",
+                 vehicle_uncharged_penalty_mode="", *, seed=0, device=0, rng="reference", **extra):
+        self._venv = SmartNanogridVecEnv(
+            1, seed=seed, device=device, rng=rng, price_model=price_model, number_of_chargers=number_of_chargers,
+            pv_system_available_in_model=pv_system_available_in_model,
+            battery_system_available_in_model=battery_system_available_in_model,
+            vehicle_to_everything=vehicle_to_everything,
+            enable_different_vehicle_battery_capacities=enable_different_vehicle_battery_capacities,
+            enable_requested_state_of_charge=enable_requested_state_of_charge, algorithm_used=algorithm_used,
+            environment_mode=environment_mode, time_interval=time_interval, charging_mode=charging_mode,
+            vehicle_uncharged_penalty_mode=vehicle_uncharged_penalty_mode, **extra)
+        self.observation_space = self._venv.observation_space
+        self.action_space = self._venv.action_space
+        self.NUMBER_OF_CHARGERS = self._venv.settings.number_of_chargers
+        self.TIME_INTERVAL = self._venv.settings.time_interval
+        self.simulated_single_day = False
+        self.timestep = None
+
+    def reset(self, generate_new_initial_values=True, algorithm_used="", environment_mode="", **kwargs):
+        """smart_nanogrid_environment.py:320-360 (gym-0.26 `seed=`/`options=` are accepted and ignored,
+        as the reference swallows them in **kwargs)."""
+        obs = self._venv.reset(generate_new_initial_values, algorithm_used, environment_mode,
+                               **{k: v for k, v in kwargs.items() if k not in ("seed", "options")})
+        self.simulated_single_day = False
+        self.timestep = 0
+        return obs[0], {}
+
+    def step(self, actions):
+        """smart_nanogrid_environment.py:149-197.  After the day ends call reset() (the reference would
+        silently re-run the day on its mutated arrays; this raises instead)."""
+        if self.simulated_single_day:
+            raise RuntimeError("the simulated day is over: call reset()")
+        v = self._venv
+        v._act_h.numpy()[0] = np.asarray(actions, dtype=np.float32).reshape(-1)
+        with torch.cuda.device(v.device):
+            v.actions_d.copy_(v._act_h, non_blocking=True)
+            obs_d, rew_d, done_d = v.step_tensors(v.actions_d)
+            v._obs_h.copy_(obs_d, non_blocking=True)
+            v._rew_h.copy_(rew_d, non_blocking=True)
+            v._done_h.copy_(done_d, non_blocking=True)
+            v._flags_h.copy_(v.flags_d, non_blocking=True)
+            torch.cuda.current_stream(v.device).synchronize()
+        v._raise_flags(v._flags_h.numpy())
+        terminated = bool(v._done_h.numpy()[0])
+        self.timestep = 0 if terminated else self.timestep + 1
+        self.simulated_single_day = terminated
+        return v._obs_h.numpy()[0].copy(), np.float64(v._rew_h.numpy()[0]), terminated, False, {}
+
+    def render(self, mode="human"):
+        pass
+
+    def seed(self, seed=None):
+        pass
+
+    def close(self):
+        self._venv.close()
+
+    @property
+    def unwrapped(self):
+        return self

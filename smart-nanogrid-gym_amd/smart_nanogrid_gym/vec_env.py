@@ -1,0 +1,369 @@
+"""Batched SmartNanogridEnv: num_envs independent copies of the reference environment
+stepped by one fused HIP kernel per timestep (libsng.so).
+
+`SmartNanogridVecEnv` duck-types stable-baselines3's VecEnv (reset / step_async /
+step_wait / num_envs / observation_space / action_space / get_attr / set_attr /
+env_method / env_is_wrapped / seed / close) with the DummyVecEnv conventions: automatic
+reset at the end of the day and the final observation in infos[i]['terminal_observation'].
+`reset_tensors` / `step_tensors` keep everything on the GPU for device-resident RL loops.
+
+Reference behaviour mirrored per env (smart_nanogrid_gym/envs/smart_nanogrid_environment.py):
+  reset()  -> new day, t = 0, BESS state of charge carried over (:320-360)
+  step(a)  -> (obs float32, reward = -total cost float64, terminated, truncated=False, {}) (:149-197)
+  errors   -> the reference's ValueErrors, raised after the step that hit them
+"""
+import ctypes
+import warnings
+
+import numpy as np
+
+from . import _native
+from ._native import check, lib
+from .settings import (BESS_ABOVE_ONE, NEGATIVE_DEMAND, WRONG_CHARGING_MODE, WRONG_PENALTY_MODE, EnvSettings)
+from .spaces import make_spaces
+
+try:
+    import torch
+except Exception:  # pragma: no cover
+    torch = None
+
+SLOTS = 25
+
+
+def _stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class SmartNanogridVecEnv:
+    """num_envs parallel SmartNanogridEnv-v0 environments on one GPU.
+
+    Parameters (besides the reference's own keyword arguments):
+      seed   -- env i behaves like the reference after `np.random.seed(seed + i); random.seed(seed + i)`
+      device -- HIP device index
+      rng    -- 'reference' (host MT19937 streams, reference-exact days) or 'device' (Philox on the GPU)
+      info   -- True: also fill the per-step diagnostics (grid power, BESS SoC, penalties ...)
+    """
+
+    metadata = {"render_modes": []}
+
+    def __init__(self, num_envs=1, *, seed=0, device=0, rng="reference", info=False, **env_kwargs):
+        if torch is None or not torch.cuda.is_available():
+            raise RuntimeError("SmartNanogridVecEnv needs a HIP device (torch.cuda unavailable)")
+        self.settings = EnvSettings(**env_kwargs)
+        self.num_envs = int(num_envs)
+        self.observation_space, self.action_space = make_spaces(self.settings)
+        self.device = torch.device("cuda", device)
+        self.rng_mode = _native.RNG_DEVICE if rng == "device" else _native.RNG_REFERENCE
+        self._seed = int(seed)
+        cfg = self.settings.to_native()
+        h = ctypes.c_void_p()
+        check(lib().sng_create(ctypes.byref(cfg), device, self.num_envs, self._seed, ctypes.byref(h)))
+        self._h = h
+        dims = _native.SngDims()
+        check(lib().sng_get_dims(h, ctypes.byref(dims)), h)
+        self.obs_dim, self.act_dim, self.timesteps = dims.obs_dim, dims.act_dim, dims.timesteps
+        E = self.num_envs
+        dev = self.device
+        self.actions_d = torch.zeros((E, self.act_dim), dtype=torch.float32, device=dev)
+        self.obs_d = torch.zeros((E, self.obs_dim), dtype=torch.float32, device=dev)
+        self.reward_d = torch.zeros(E, dtype=torch.float64, device=dev)
+        self.done_d = torch.zeros(E, dtype=torch.uint8, device=dev)
+        self.flags_d = torch.zeros(E, dtype=torch.int32, device=dev)
+        self.return_d = torch.zeros(E, dtype=torch.float64, device=dev)
+        self.info_d = {}
+        if info:
+            self.info_d = {f: torch.zeros(E, dtype=torch.float64, device=dev) for f in _native.INFO_FIELDS}
+        self._info = _native.SngInfo()
+        for f, t in self.info_d.items():
+            setattr(self._info, f, t.data_ptr())
+        self._info.flags = self.flags_d.data_ptr()
+        self._info.episode_return = self.return_d.data_ptr()
+        # pinned host mirrors for the numpy (SB3) path
+        pin = dict(pin_memory=True)
+        self._act_h = torch.zeros((E, self.act_dim), dtype=torch.float32, **pin)
+        self._obs_h = torch.zeros((E, self.obs_dim), dtype=torch.float32, **pin)
+        self._rew_h = torch.zeros(E, dtype=torch.float64, **pin)
+        self._done_h = torch.zeros(E, dtype=torch.uint8, **pin)
+        self._flags_h = torch.zeros(E, dtype=torch.int32, **pin)
+        self._pending = None
+        self._warned_breakpoint = False
+        self.closed = False
+
+    # ------------------------------------------------------------------ lifecycle
+    def close(self):
+        if not self.closed and getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            lib().sng_destroy(self._h)
+            self._h = None
+        self.closed = True
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def timestep(self):
+        return lib().sng_get_timestep(self._h)
+
+    def _check_mode(self):
+        if self.settings.penalty_mode is None:   # charging_station.py:59-60 raises inside reset()
+            raise ValueError(WRONG_PENALTY_MODE)
+
+    # ------------------------------------------------------------------ device-resident API
+    def reset_tensors(self, rng=None):
+        """New day for every env; returns the t=0 observations (device tensor [E, obs_dim])."""
+        self._check_mode()
+        mode = self.rng_mode if rng is None else (_native.RNG_DEVICE if rng == "device" else _native.RNG_REFERENCE)
+        with torch.cuda.device(self.device):
+            self.return_d.zero_()
+            check(lib().sng_reset(self._h, mode, ctypes.c_void_p(self.obs_d.data_ptr()),
+                                  _stream_handle(self.device)), self._h)
+        return self.obs_d
+
+    def step_tensors(self, actions):
+        """One step for every env from device actions [E, act_dim] float32.
+        Returns (obs [E, obs_dim] f32, reward [E] f64, done [E] u8) device tensors, no auto-reset."""
+        if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
+            actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        if tuple(actions.shape) != (self.num_envs, self.act_dim):
+            raise ValueError(f"actions must have shape {(self.num_envs, self.act_dim)}")
+        with torch.cuda.device(self.device):
+            check(lib().sng_step(self._h, ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(self.obs_d.data_ptr()),
+                                 ctypes.c_void_p(self.reward_d.data_ptr()), ctypes.c_void_p(self.done_d.data_ptr()),
+                                 ctypes.byref(self._info), _stream_handle(self.device)), self._h)
+        return self.obs_d, self.reward_d, self.done_d
+
+    def reset_from_initial_values(self, initial_values, pv_ratio, restore_requested_soc=False):
+        """reset(generate_new_initial_values=False) (smart_nanogrid_environment.py:362-366).
+
+        initial_values: one dict (broadcast to all envs) or a list of num_envs dicts in the
+        reference's initial_values.json schema (charging_station.py:164-180).  The reference's
+        load_initial_values (charging_station.py:119-136) does not restore 'Requested_SOC'
+        (left at 0); restore_requested_soc=True uses the recorded values instead.
+        """
+        self._check_mode()
+        E, N = self.num_envs, self.settings.number_of_chargers
+        items = initial_values if isinstance(initial_values, (list, tuple)) else [initial_values] * E
+        if len(items) != E:
+            raise ValueError("need one initial_values dict per env")
+        V = max(1, max(len(a) for d in items for a in d["Arrivals"]))
+        soc = np.zeros((E, N, SLOTS))
+        occ = np.zeros((E, N, SLOTS))
+        cap = np.zeros((E, N, SLOTS))
+        req = np.zeros((E, N, SLOTS))
+        arr = np.full((E, N, V), -1, np.int32)
+        dep = np.full((E, N, V), -1, np.int32)
+        for i, d in enumerate(items):
+            soc[i] = np.asarray(d["SOC"], np.float64)
+            occ[i] = np.asarray(d["Charger_occupancy"], np.float64)
+            cap[i] = np.asarray(d["Vehicle_capacities"], np.float64)
+            if restore_requested_soc and "Requested_SOC" in d:
+                req[i] = np.asarray(d["Requested_SOC"], np.float64)
+            for c in range(N):
+                arr[i, c, :len(d["Arrivals"][c])] = d["Arrivals"][c]
+                dep[i, c, :len(d["Departures"][c])] = d["Departures"][c]
+        ratio = np.broadcast_to(np.asarray(pv_ratio, np.float64), (E,)).copy()
+        return self.reset_from_arrays(soc, occ, cap, req, arr, dep, ratio)
+
+    def reset_from_arrays(self, soc, occupancy, capacity, requested_soc, arrivals, departures, pv_ratio):
+        """Start a day from explicit reference-layout arrays ([E, N, 25] / [E, N, V], -1 padded)."""
+        self._check_mode()
+        arrs = [np.ascontiguousarray(a, np.float64) for a in (soc, occupancy, capacity, requested_soc)]
+        ai = np.ascontiguousarray(arrivals, np.int32)
+        di = np.ascontiguousarray(departures, np.int32)
+        ratio = np.ascontiguousarray(pv_ratio, np.float64)
+        sc = _native.SngScenario()
+        sc.slots = SLOTS
+        sc.max_vehicles = ai.shape[-1]
+        sc.soc, sc.occupancy, sc.capacity, sc.requested_soc = [a.ctypes.data_as(_native.c_double_p) for a in arrs]
+        sc.arrivals = ai.ctypes.data_as(_native.c_int32_p)
+        sc.departures = di.ctypes.data_as(_native.c_int32_p)
+        sc.pv_ratio = ratio.ctypes.data_as(_native.c_double_p)
+        with torch.cuda.device(self.device):
+            self.return_d.zero_()
+            check(lib().sng_reset_from_scenario(self._h, ctypes.byref(sc), ctypes.c_void_p(self.obs_d.data_ptr()),
+                                                _stream_handle(self.device)), self._h)
+            torch.cuda.current_stream(self.device).synchronize()
+        return self._obs_to_host()
+
+    # ------------------------------------------------------------------ SB3 VecEnv API
+    def reset(self, generate_new_initial_values=True, algorithm_used="", environment_mode="", **kwargs):
+        if algorithm_used:
+            self.settings.algorithm_used = algorithm_used
+        if environment_mode:
+            self.settings.environment_mode = environment_mode
+        if not generate_new_initial_values:
+            if "initial_values" not in kwargs:
+                raise ValueError("reset(generate_new_initial_values=False) needs initial_values=<dict> "
+                                 "(and pv_ratio=...) in this implementation")
+            return self.reset_from_initial_values(kwargs["initial_values"], kwargs.get("pv_ratio", 1.0),
+                                                  kwargs.get("restore_requested_soc", False))
+        self.reset_tensors()
+        return self._obs_to_host()
+
+    def step_async(self, actions):
+        self._pending = actions
+
+    def step_wait(self):
+        actions = self._pending
+        self._pending = None
+        E = self.num_envs
+        a = np.asarray(actions, dtype=np.float32).reshape(E, self.act_dim)
+        self._act_h.numpy()[...] = a
+        stream = torch.cuda.current_stream(self.device)
+        with torch.cuda.device(self.device):
+            self.actions_d.copy_(self._act_h, non_blocking=True)
+            self.step_tensors(self.actions_d)
+            self._obs_h.copy_(self.obs_d, non_blocking=True)
+            self._rew_h.copy_(self.reward_d, non_blocking=True)
+            self._done_h.copy_(self.done_d, non_blocking=True)
+            self._flags_h.copy_(self.flags_d, non_blocking=True)
+            stream.synchronize()
+        self._raise_flags(self._flags_h.numpy())
+        obs = self._obs_h.numpy().copy()
+        rewards = self._rew_h.numpy().copy()
+        dones = self._done_h.numpy().astype(bool)
+        infos = [{} for _ in range(E)]
+        flags = self._flags_h.numpy()
+        if flags.any():
+            for i in np.nonzero(flags & _native.FLAG_V2X_BREAKPOINT)[0]:
+                infos[i]["v2x_breakpoint"] = True
+        if dones.any():
+            for i in range(E):
+                infos[i]["terminal_observation"] = obs[i]
+                infos[i]["TimeLimit.truncated"] = False
+            obs = self.reset()
+        return obs, rewards, dones, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def seed(self, seed=None):
+        """The reference's seed() is a no-op (:371-374); streams are fixed at construction."""
+        return [None if seed is None else seed + i for i in range(self.num_envs)]
+
+    def render(self, mode="human"):
+        return None
+
+    def get_attr(self, attr_name, indices=None):
+        return [getattr(self.settings, attr_name, getattr(self, attr_name, None)) for _ in self._idx(indices)]
+
+    def set_attr(self, attr_name, value, indices=None):
+        setattr(self.settings, attr_name, value)
+
+    def env_method(self, method_name, *args, indices=None, **kwargs):
+        return [getattr(self, method_name)(*args, **kwargs) for _ in self._idx(indices)][:1] * len(self._idx(indices))
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False for _ in self._idx(indices)]
+
+    def get_images(self):
+        return []
+
+    def _idx(self, indices):
+        if indices is None:
+            return range(self.num_envs)
+        if isinstance(indices, int):
+            return [indices]
+        return indices
+
+    # ------------------------------------------------------------------ helpers
+    def _obs_to_host(self):
+        self._obs_h.copy_(self.obs_d, non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return self._obs_h.numpy().copy()
+
+    def _raise_flags(self, flags):
+        if not flags.any():
+            return
+        f = int(np.bitwise_or.reduce(flags))
+        if f & _native.FLAG_NEGATIVE_DEMAND:
+            raise ValueError(NEGATIVE_DEMAND)
+        if f & _native.FLAG_CHARGING_MODE:
+            raise ValueError(WRONG_CHARGING_MODE)
+        if f & _native.FLAG_BESS_SOC_ABOVE_1:
+            raise ValueError(BESS_ABOVE_ONE)
+        if f & _native.FLAG_V2X_BREAKPOINT and not self._warned_breakpoint:
+            self._warned_breakpoint = True
+            warnings.warn("V2X total power demand < 0: the reference stops in breakpoint() here "
+                          "(central_management_system.py:160-165); continuing", RuntimeWarning)
+
+    def last_info(self):
+        """Per-step diagnostics of the last step (numpy, names of the reference results dict)."""
+        torch.cuda.current_stream(self.device).synchronize()
+        out = {k: v.cpu().numpy() for k, v in self.info_d.items()}
+        out["flags"] = self.flags_d.cpu().numpy()
+        out["episode_return"] = self.return_d.cpu().numpy()
+        return out
+
+    def battery_state_of_charge(self):
+        out = np.zeros(self.num_envs)
+        check(lib().sng_get_battery_soc(self._h, out.ctypes.data_as(_native.c_double_p)), self._h)
+        return out
+
+    def set_battery_state_of_charge(self, soc):
+        v = np.ascontiguousarray(np.broadcast_to(np.asarray(soc, np.float64), (self.num_envs,)))
+        check(lib().sng_set_battery_soc(self._h, v.ctypes.data_as(_native.c_double_p)), self._h)
+
+    def pv_ratio(self):
+        out = np.zeros(self.num_envs)
+        check(lib().sng_get_pv_ratio(self._h, out.ctypes.data_as(_native.c_double_p)), self._h)
+        return out
+
+    def vehicle_state_of_charge(self):
+        out = np.zeros((self.num_envs, self.settings.number_of_chargers))
+        check(lib().sng_get_vehicle_soc(self._h, out.ctypes.data_as(_native.c_double_p)), self._h)
+        return out
+
+    def tables(self):
+        n = ctypes.c_int32()
+        irr = np.zeros(512)
+        pv = np.zeros(512)
+        price = np.zeros(48)
+        mx = ctypes.c_double()
+        pmx = ctypes.c_double()
+        P = _native.c_double_p
+        check(lib().sng_get_tables(self._h, irr.ctypes.data_as(P), ctypes.byref(mx), pv.ctypes.data_as(P),
+                                   price.ctypes.data_as(P), ctypes.byref(pmx), ctypes.byref(n)), self._h)
+        return dict(irr=irr[:n.value], irr_max=mx.value, pv_power=pv[:n.value], price=price, price_max=pmx.value)
+
+
+class EpisodeGraph:
+    """A whole day (device-RNG reset + T fused steps) captured once as a hipGraph and
+    replayed; actions come from a device tensor [T, E, act_dim]."""
+
+    def __init__(self, venv, actions, with_reset=True):
+        self.venv = venv
+        self.actions = actions.contiguous()
+        g = ctypes.c_void_p()
+        with torch.cuda.device(venv.device):
+            check(lib().sng_graph_create(venv._h, ctypes.c_void_p(self.actions.data_ptr()),
+                                         ctypes.c_void_p(venv.obs_d.data_ptr()),
+                                         ctypes.c_void_p(venv.reward_d.data_ptr()),
+                                         ctypes.c_void_p(venv.done_d.data_ptr()), ctypes.byref(venv._info),
+                                         int(with_reset), ctypes.byref(g)), venv._h)
+        self._g = g
+
+    def launch(self, stream=None):
+        s = _stream_handle(self.venv.device) if stream is None else ctypes.c_void_p(stream)
+        check(lib().sng_graph_launch(self._g, s), self.venv._h)
+
+    def step_kernel_ms(self):
+        """Device time of each step kernel in the latest replay (HIP events inside the graph)."""
+        out = np.zeros(self.venv.timesteps, np.float32)
+        check(lib().sng_graph_step_times(self._g, out.ctypes.data_as(_native.c_float_p), out.size), self.venv._h)
+        return out
+
+    def close(self):
+        if getattr(self, "_g", None):
+            lib().sng_graph_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,264 @@
+"""GPU parity: the HIP step/reset path (through the C ABI) against the reference's golden
+vectors and the CPU oracle.  All tests need an MI355X.
+
+Tolerances: observations are compared bit for bit.  Rewards are compared bit for bit
+against the oracle in x*x mode (the GPU squares with x*x); against the reference's own
+numbers (libm pow(x, 2), which is off by one ulp on ~0.1 % of inputs) within 1e-12
+relative -- far inside the 1e-5 the north star allows.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle as O
+from golden_util import case, cases, kat
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from smart_nanogrid_gym import EpisodeGraph, SmartNanogridEnv, SmartNanogridVecEnv  # noqa: E402
+
+INFO_MAP = {"grid_power": "grid_power", "total_charging_power": "p_charge",
+            "total_discharging_power": "p_discharge", "battery_state_of_charge": "bess_soc",
+            "total_vehicle_penalty": "pen_vehicle", "total_battery_penalty": "pen_battery",
+            "grid_energy_cost": "grid_cost", "total_cost": "total_cost", "utilized_solar_energy": "solar_power",
+            "battery_power_value": "bess_power", "battery_calculated_power": "bess_calc_power",
+            "nonexistent_vehicle_penalty": "nonexistent", "initial_battery_soc": "bess_initial_soc"}
+
+
+def rel_close(a, b, tol=1e-12):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return np.all(np.abs(a - b) <= tol * np.maximum(1.0, np.abs(b)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _square_mode():
+    O.lib().orc_set_square_mode.argtypes = [ctypes.c_int]
+    yield
+    O.lib().orc_set_square_mode(0)
+
+
+@pytest.mark.parametrize("name", [m["name"] for m in cases()])
+def test_golden_cases_reference_rng_end_to_end(name):
+    """Env seeded like the reference (np.random.seed(s); random.seed(s)): reset, step through every
+    recorded day with the recorded actions, auto-reset between days (BESS carried over)."""
+    meta, d = case(name)
+    venv = SmartNanogridVecEnv(1, seed=meta["seed"], rng="reference", info=True, **meta["kwargs"])
+    obs = venv.reset()
+    for ep in range(meta["n_episodes"]):
+        np.testing.assert_array_equal(obs[0], d["obs_reset"][ep])
+        for t in range(meta["T"]):
+            obs, rew, dones, infos = venv.step(d["actions"][ep][t][None])
+            info = venv.last_info()
+            final = infos[0].get("terminal_observation", obs[0])
+            np.testing.assert_array_equal(final, d["obs"][ep][t], err_msg=f"ep{ep} t{t}")
+            assert rel_close(rew[0], d["reward"][ep][t]), (ep, t, rew[0], d["reward"][ep][t])
+            assert bool(dones[0]) == bool(d["done"][ep][t])
+            for k, g in INFO_MAP.items():
+                assert rel_close(info[k][0], d[g][ep][t]), (k, ep, t, info[k][0], d[g][ep][t])
+            assert bool(info["flags"][0] & 8) == bool(d["breakpoint"][ep][t])
+    venv.close()
+
+
+@pytest.mark.parametrize("name", ["bpv_sparse_n10", "bpv_dense_req_n50", "v2x_bpv_n10", "bpv_2h_n10"])
+def test_golden_cases_injected_scenario(name):
+    """reset_from_arrays with the recorded day (reference layout) + recorded BESS SoC."""
+    meta, d = case(name)
+    venv = SmartNanogridVecEnv(1, seed=0, info=True, **meta["kwargs"])
+    for ep in range(meta["n_episodes"]):
+        venv.set_battery_state_of_charge(d["bess_soc_reset"][ep])
+        obs = venv.reset_from_arrays(d["soc0"][ep][None], d["occ"][ep][None], d["cap"][ep][None],
+                                     d["req"][ep][None], d["arrivals"][ep][None], d["departures"][ep][None],
+                                     np.array([d["ratio"][ep]]))
+        np.testing.assert_array_equal(obs[0], d["obs_reset"][ep])
+        for t in range(meta["T"]):
+            o, r, dn = venv.step_tensors(torch.from_numpy(d["actions"][ep][t][None]).to(venv.device))
+            np.testing.assert_array_equal(o.cpu().numpy()[0], d["obs"][ep][t])
+            assert rel_close(r.cpu().numpy()[0], d["reward"][ep][t])
+    venv.close()
+
+
+@pytest.mark.parametrize("sub", ["single_prediction_files", "training_files"])
+def test_recorded_ppo_episode_replay(sub):
+    """The reference's recorded PPO day (NumPy 1.24 promotion, 0.8 grid-cost weight) replayed on GPU."""
+    k = kat(sub)
+    iv, pr = k["iv"], k["pr"]
+    venv = SmartNanogridVecEnv(1, info=True, number_of_chargers=k["N"], time_interval="1h", charging_mode="bounded",
+                               vehicle_uncharged_penalty_mode="sparse", numpy_legacy_promotion=True,
+                               grid_cost_weight=0.8)
+    venv.set_battery_state_of_charge(k["bess_soc0"])
+    venv.reset_from_initial_values(iv, k["ratio"], restore_requested_soc=True)
+    for t in range(24):
+        venv.step_tensors(torch.from_numpy(k["actions"][t][None]).to(venv.device))
+        info = venv.last_info()
+        assert rel_close(info["grid_power"][0], pr["Grid_power"][t])
+        assert info["battery_state_of_charge"][0] == pr["Battery_state_of_charge"][t]
+        assert rel_close(info["total_cost"][0], pr["Total_cost"][t])
+        assert rel_close(info["total_vehicle_penalty"][0], pr["Total_vehicle_penalties"][t])
+    np.testing.assert_array_equal(venv.vehicle_state_of_charge()[0], np.array(pr["SOC"])[:, 23])
+    venv.close()
+
+
+def _oracle_batch(kw, seed, idx):
+    cfg = O.OracleConfig(**kw)
+    return cfg, [O.OracleEnv(cfg, seed + int(i)) for i in idx]
+
+
+@pytest.mark.parametrize("E,N,mode", [(4096, 10, "sparse"), (4096, 10, "dense"), (1024, 50, "sparse"),
+                                      (1000, 4, "on_departure"), (333, 1, "sparse")])
+def test_batched_reference_rng_vs_oracle_bit_exact(E, N, mode):
+    """Config 2 (4,096 envs x 10 chargers x 24 steps): every env against the oracle seeded base+i,
+    two consecutive days, random actions with 20 % exact zeros."""
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode=mode)
+    seed = 1000 + N
+    O.lib().orc_set_square_mode(1)
+    venv = SmartNanogridVecEnv(E, seed=seed, rng="reference", **kw)
+    cfg, envs = _oracle_batch(kw, seed, range(E))
+    rng = np.random.default_rng(E + N)
+    for day in range(2):
+        obs = venv.reset() if day == 0 else obs
+        np.testing.assert_array_equal(obs, np.stack([e.reset() for e in envs]))
+        for t in range(cfg.T):
+            a = rng.uniform(venv.action_space.low, venv.action_space.high, (E, venv.act_dim)).astype(np.float32)
+            a[rng.random(a.shape) < 0.2] = 0
+            obs, rew, dones, infos = venv.step(a)
+            outs = [e.step(a[i]) for i, e in enumerate(envs)]
+            ref_obs = np.stack([o[0] for o in outs])
+            got = np.stack([inf.get("terminal_observation", obs[i]) for i, inf in enumerate(infos)])
+            np.testing.assert_array_equal(got, ref_obs, err_msg=f"day{day} t{t}")
+            np.testing.assert_array_equal(rew, np.array([o[1] for o in outs]))
+            assert dones.all() == (t == cfg.T - 1)
+    np.testing.assert_array_equal(venv.battery_state_of_charge(), np.array([e.bess_soc for e in envs]))
+    venv.close()
+
+
+def test_full_size_sampled_parity_65536():
+    """Config 3 size (65,536 envs x 10 chargers) with reference RNG: 512 sampled envs against the oracle,
+    plus size-independent invariants on all envs."""
+    E, N, seed = 65536, 10, 99
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    O.lib().orc_set_square_mode(1)
+    venv = SmartNanogridVecEnv(E, seed=seed, rng="reference", info=True, **kw)
+    idx = np.random.default_rng(5).choice(E, 512, replace=False)
+    cfg, envs = _oracle_batch(kw, seed, idx)
+    obs = venv.reset()
+    np.testing.assert_array_equal(obs[idx], np.stack([e.reset() for e in envs]))
+    g = torch.Generator(device=venv.device).manual_seed(3)
+    low = torch.tensor(venv.action_space.low, device=venv.device)
+    high = torch.tensor(venv.action_space.high, device=venv.device)
+    total = torch.zeros(E, dtype=torch.float64, device=venv.device)
+    for t in range(cfg.T):
+        a = low + (high - low) * torch.rand((E, venv.act_dim), generator=g, device=venv.device)
+        a = torch.where(torch.rand(a.shape, generator=g, device=venv.device) < 0.2, torch.zeros_like(a), a)
+        o, r, dn = venv.step_tensors(a)
+        total += r
+        ah = a.cpu().numpy()
+        outs = [e.step(ah[i]) for e, i in zip(envs, idx)]
+        oh = o.cpu().numpy()
+        np.testing.assert_array_equal(oh[idx], np.stack([x[0] for x in outs]))
+        np.testing.assert_array_equal(r.cpu().numpy()[idx], np.array([x[1] for x in outs]))
+        # invariants on every env
+        soc = oh[:, 8:8 + N]
+        assert soc.min() >= 0 and soc.max() <= 1
+        assert (r.cpu().numpy() <= 0).all()
+        info = venv.last_info()
+        assert (info["battery_state_of_charge"] >= 0).all() and (info["battery_state_of_charge"] <= 1).all()
+        assert (info["flags"] == 0).all()
+    ret = venv.last_info()["episode_return"]
+    assert rel_close(ret, total.cpu().numpy(), 1e-9)
+    venv.close()
+
+
+def test_device_rng_day_distribution_and_invariants():
+    """GPU Philox days: same distributions as the reference generator (oracle MT draws)."""
+    E, N = 65536, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    venv = SmartNanogridVecEnv(E, seed=7, rng="device", info=True, **kw)
+    obs = venv.reset()
+    occ0 = (obs[:, 8 + N:8 + 2 * N] > 0).mean()
+    soc_occ = obs[:, 8:8 + N][obs[:, 8 + N:8 + 2 * N] > 0]
+    ratio = venv.pv_ratio()
+    # oracle statistics over 4,000 reference-RNG envs
+    cfg = O.OracleConfig(**kw)
+    ref_occ0, ref_soc, ref_ratio = [], [], []
+    for i in range(4000):
+        e = O.OracleEnv(cfg, 50_000 + i)
+        o = e.reset()
+        m = o[8 + N:8 + 2 * N] > 0
+        ref_occ0.append(m.mean())
+        ref_soc.extend(o[8:8 + N][m])
+        ref_ratio.append(e.ratio)
+    assert abs(occ0 - np.mean(ref_occ0)) < 0.01
+    assert abs(soc_occ.mean() - np.mean(ref_soc)) < 0.01
+    assert abs(ratio.mean() - np.mean(ref_ratio)) < 0.02
+    assert set(np.unique(np.round(ratio * 100))).issubset(set(range(181)))
+    occupancy = []
+    g = torch.Generator(device=venv.device).manual_seed(1)
+    for t in range(24):
+        a = torch.rand((E, venv.act_dim), generator=g, device=venv.device)
+        a[:, -1] = a[:, -1] * 2 - 1
+        o, r, dn = venv.step_tensors(a)
+        oh = o.cpu().numpy()
+        occupancy.append((oh[:, 8 + N:8 + 2 * N] > 0).mean())
+        assert oh[:, 8:8 + N].min() >= 0 and oh[:, 8:8 + N].max() <= 1
+        assert (venv.last_info()["flags"] == 0).all()
+    # mean occupancy over the day, reference generator: ~0.71 at N=10
+    assert 0.66 < np.mean(occupancy) < 0.76
+    venv.close()
+
+
+def test_episode_graph_matches_eager_device_rng():
+    E, N = 8192, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    a = SmartNanogridVecEnv(E, seed=11, rng="device", **kw)
+    b = SmartNanogridVecEnv(E, seed=11, rng="device", **kw)
+    graph = EpisodeGraph(b, acts)
+    for day in range(3):
+        a.reset_tensors()
+        for t in range(24):
+            oa, ra, da = a.step_tensors(acts[t])
+        graph.launch()
+        torch.cuda.synchronize()
+        assert torch.equal(oa, b.obs_d) and torch.equal(ra, b.reward_d) and torch.equal(da, b.done_d)
+        assert torch.equal(a.return_d, b.return_d)
+    graph.close()
+    a.close()
+    b.close()
+
+
+def test_single_env_gym_surface():
+    env = SmartNanogridEnv(number_of_chargers=4, time_interval="1h", charging_mode="bounded",
+                           vehicle_uncharged_penalty_mode="sparse", seed=12)
+    meta, d = case("bpv_sparse_n4")
+    obs, info = env.reset()
+    assert info == {} and obs.dtype == np.float32 and obs.shape == env.observation_space.shape
+    np.testing.assert_array_equal(obs, d["obs_reset"][0])
+    for t in range(24):
+        obs, r, term, trunc, info = env.step(d["actions"][0][t])
+        np.testing.assert_array_equal(obs, d["obs"][0][t])
+        assert isinstance(r, np.float64) and trunc is False and term == (t == 23)
+    with pytest.raises(RuntimeError):
+        env.step(d["actions"][0][0])
+    env.close()
+
+
+def test_reference_errors_are_raised():
+    env = SmartNanogridVecEnv(2, number_of_chargers=3, time_interval="1h", charging_mode="",
+                              vehicle_uncharged_penalty_mode="sparse")
+    env.reset()
+    with pytest.raises(ValueError, match="charging mode"):
+        for _ in range(24):
+            env.step(np.ones((2, 4), np.float32))
+    env.close()
+    env = SmartNanogridVecEnv(2, number_of_chargers=3, time_interval="1h", charging_mode="bounded",
+                              vehicle_uncharged_penalty_mode="")
+    with pytest.raises(ValueError, match="penalty mode"):
+        env.reset()
+    env.close()

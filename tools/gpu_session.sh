@@ -1,0 +1,32 @@
+#!/bin/bash
+# One GPU session: tests, smoke, bench, rocprof kernel stats.  Every GPU step has its own time
+# limit; the script stops at the first fatal exit (abort/segfault/timeout), and continues past
+# ordinary test failures (exit 1) so the bench still runs.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out
+mkdir -p $OUT
+export TMPDIR=/tmp
+fatal() { case "$1" in 0|1|2|5) return 1;; *) return 0;; esac; }
+run() {  # run <name> <timeout> <cmd...>
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a $OUT/session.log
+  timeout -k 10 "$to" "$@" > $OUT/$name.log 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a $OUT/session.log
+  tail -5 $OUT/$name.log | tee -a $OUT/session.log
+  if fatal $rc; then echo "fatal exit $rc in $name; stopping" | tee -a $OUT/session.log; exit $rc; fi
+  return 0
+}
+STEPS="${STEPS:-tests smoke bench prof}"
+for s in $STEPS; do
+  case $s in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    prof)  run prof_stats 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc_write -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 ;;
+  esac
+done
+echo "=== session done" | tee -a $OUT/session.log
