@@ -195,9 +195,11 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 
 /* One full day captured as a hipGraph: [device-RNG reset] + T fused steps.  actions
  * holds T consecutive [num_envs][act_dim] blocks; obs/reward/done are overwritten every
- * step; info may be NULL.  Replays draw a new day each time. */
+ * step; info may be NULL.  Replays draw a new day each time.  flags: SNG_GRAPH_*. */
+#define SNG_GRAPH_RESET 1   /* start every replay with a device-RNG reset */
+#define SNG_GRAPH_TIMING 2  /* capture HIP events around every step kernel */
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
-                     const SngInfo *info, int with_reset, SngGraph **out);
+                     const SngInfo *info, int flags, SngGraph **out);
 int sng_graph_launch(SngGraph *graph, void *stream);
 /* Device time (ms) of each of the T step kernels in the most recent replay, measured by
  * HIP events captured around every step kernel in the graph.  Synchronises. */

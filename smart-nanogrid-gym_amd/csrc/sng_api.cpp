@@ -813,7 +813,8 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 }
 
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
-                     const SngInfo *info, int with_reset, SngGraph **out) {
+                     const SngInfo *info, int flags, SngGraph **out) {
+    const bool with_reset = (flags & SNG_GRAPH_RESET) != 0, timing = (flags & SNG_GRAPH_TIMING) != 0;
     if (!env || !actions || !obs || !reward || !done || !out) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     if (with_reset && env->i4 < 2) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
     HIP_TRY(env, hipSetDevice(env->device));
@@ -836,14 +837,14 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
         e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, cs);
         if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, cs);
     }
-    g->ev.assign(2 * (size_t)p.T, nullptr);
+    if (timing) g->ev.assign(2 * (size_t)p.T, nullptr);
     for (auto &x : g->ev)
         if (e == hipSuccess) e = hipEventCreate(&x);
     for (int t = 0; e == hipSuccess && t < p.T; ++t) {
-        e = hipEventRecord(g->ev[2 * t], cs);
+        if (timing) e = hipEventRecordWithFlags(g->ev[2 * t], cs, hipEventRecordExternal);
         if (e == hipSuccess)
             e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
-        if (e == hipSuccess) e = hipEventRecord(g->ev[2 * t + 1], cs);
+        if (e == hipSuccess && timing) e = hipEventRecordWithFlags(g->ev[2 * t + 1], cs, hipEventRecordExternal);
     }
     hipGraph_t graph = nullptr;
     hipError_t e2 = hipStreamEndCapture(cs, &graph);
@@ -887,6 +888,7 @@ int sng_graph_step_times(SngGraph *g, float *ms, int32_t n) {
     SngEnv *env = g->env;
     HIP_TRY(env, hipSetDevice(env->device));
     const int T = (int)(g->ev.size() / 2);
+    if (T == 0) return fail(env, SNG_ERR_STATE, "graph was created without SNG_GRAPH_TIMING");
     for (int t = 0; t < T && t < n; ++t) {
         HIP_TRY(env, hipEventSynchronize(g->ev[2 * t + 1]));
         HIP_TRY(env, hipEventElapsedTime(&ms[t], g->ev[2 * t], g->ev[2 * t + 1]));

@@ -61,15 +61,43 @@ __device__ __forceinline__ size_t lds_obs_offset(int act_dim) {
     return ((size_t)kWave * act_dim + 3) & ~(size_t)3;
 }
 
-// Copy `count` floats global -> LDS (or back) with 16 B per lane when the run is aligned.
+// Copy `count` floats global -> LDS with 16 B per lane when the run is aligned.  Each lane
+// issues up to K loads before the first LDS write, so the whole copy is one HBM round trip
+// when count <= K * 256 floats.
+template <int K>
 __device__ __forceinline__ void copy_in(float *__restrict__ dst, const float *__restrict__ src, int count,
                                         bool vec, int lane) {
     if (vec && (count & 3) == 0) {
         const float4 *s4 = reinterpret_cast<const float4 *>(src);
         float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int i = lane; i < (count >> 2); i += kWave) d4[i] = s4[i];
+        const int n4 = count >> 2;
+        for (int base = 0; base < n4; base += K * kWave) {
+            float4 v[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {   // clamped, unconditional: no per-element branch + wait
+                const int i = base + k * kWave + lane;
+                v[k] = s4[i < n4 ? i : n4 - 1];
+            }
+#pragma unroll
+            for (int k = 0; k < K; ++k) {   // out-of-range lanes rewrite the last element (same value)
+                const int i = base + k * kWave + lane;
+                d4[i < n4 ? i : n4 - 1] = v[k];
+            }
+        }
     } else {
-        for (int i = lane; i < count; i += kWave) dst[i] = src[i];
+        for (int base = 0; base < count; base += 4 * K * kWave) {
+            float v[4 * K];
+#pragma unroll
+            for (int k = 0; k < 4 * K; ++k) {
+                const int i = base + k * kWave + lane;
+                v[k] = src[i < count ? i : count - 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4 * K; ++k) {
+                const int i = base + k * kWave + lane;
+                dst[i < count ? i : count - 1] = v[k];
+            }
+        }
     }
 }
 
@@ -101,13 +129,18 @@ __device__ __forceinline__ int write_obs_header(float *o, const Params &p, const
 
 // ---------------------------------------------------------------------------------
 // The fused step: SmartNanogridEnv.step(actions) for 64 envs per workgroup.
-// NC = compile-time charger count (0: runtime p.n).
+// NC   = compile-time charger count (0: runtime p.n);
+// DIAG = also write the per-step diagnostics (SngInfo arrays).
+// All per-charger loads of a batch of CH chargers are issued before any of them is used
+// (and the first batch before the action staging wait), so a wavefront keeps
+// 3*CH + 2 independent HBM requests in flight instead of one round trip per charger.
 // ---------------------------------------------------------------------------------
-template <int NC>
+template <int NC, bool DIAG>
 __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, InfoPtrs info,
                                                      const float *__restrict__ act, float *__restrict__ obs,
                                                      double *__restrict__ reward, uint8_t *__restrict__ done,
                                                      int64_t E, int t, int vec_io) {
+    constexpr int CH = (NC > 0 && NC <= 16) ? NC : 8;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int n = NC ? NC : p.n;
     const int A = p.act_dim, O = p.obs_dim;
@@ -118,14 +151,37 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
     const bool live = lane < nblk;
     float *s_act = lds;
     float *s_obs = lds + lds_obs_offset(A);
+    const uint32_t *__restrict__ word = s.word;
+    const double *__restrict__ auxv = s.aux;
+    double *__restrict__ socv = s.soc;
+    const size_t tbase = (size_t)t * n;
 
-    copy_in(s_act, act + e0 * A, nblk * A, vec_io != 0, lane);
+    uint32_t w[CH];
+    double aux[CH], run[CH];
+    auto load_batch = [&](int c0) {
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+            const int c = c0 + j;
+            if (c < n) {
+                const size_t idx = (tbase + c) * (size_t)E + e;
+                w[j] = word[idx];
+                aux[j] = auxv[idx];
+                run[j] = socv[(size_t)c * E + e];
+            }
+        }
+    };
+
+    double ratio = 0.0, bess = 0.0;
+    if (live) {
+        ratio = s.ratio[e];
+        if (p.bess) bess = s.bess[e];
+        load_batch(0);
+    }
+    copy_in<(NC > 0 && NC < 16) ? 4 : 8>(s_act, act + e0 * A, nblk * A, vec_io != 0, lane);
     __syncthreads();
 
     if (live) {
         const Tables *tb = s.tables;
-        const double ratio = s.ratio[e];
-        double bess = p.bess ? s.bess[e] : 0.0;
         const float *a_row = s_act + lane * A;
         float *o_row = s_obs + lane * O;
         const int k_soc = (p.pv ? 8 : 4);
@@ -136,67 +192,69 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
         neg.init();
         double pen_v = 0.0, nonexist = 0.0;
         uint32_t fl = 0;
-        const size_t tbase = (size_t)t * n;
+        for (int c0 = 0; c0 < n; c0 += CH) {
+            if (c0 > 0) load_batch(c0);
 #pragma unroll
-        for (int c = 0; c < n; ++c) {
-            const size_t idx = (tbase + c) * (size_t)E + e;
-            const uint32_t w = s.word[idx];
-            const double aux = s.aux[idx];
-            double run = s.soc[(size_t)c * E + e];
-            const float a = a_row[c];
+            for (int j = 0; j < CH; ++j) {
+                const int c = c0 + j;
+                if (c >= n) break;
+                const uint32_t wj = w[j];
+                double r = run[j];
+                const float a = a_row[c];
 
-            // penalise_charging_vehicles_outside_bounds (penaliser.py:39-57, 71-87): the vehicle's
-            // SoC and requested SoC at python index t-1; Python sum() order over the list.
-            if (t > 0 && (w & W_PEN)) {
-                const double req = p.req_stream ? s.req[idx] : 1.0;
-                const double margin = 0.05 * req;
-                if (run < req - margin) {
-                    const double d = (req - run) * 10;
-                    pen_v += d * d;
-                }
-            }
-
-            // Charger.charge_or_discharge_vehicle (charger.py:37-56, 58-94, 108-144)
-            double pw = 0.0;
-            if (w & W_OCC) {
-                const double prev = (w & W_STATIC) ? aux : run;
-                const double cap = (double)((w >> W_CAP_SHIFT) & 0xffu);
-                double nsoc = prev;
-                if (a == 0.0f) {
-                    nsoc = prev;
-                } else if (!p.bounded) {
-                    fl |= SNG_FLAG_CHARGING_MODE;
-                } else {
-                    double pc, change;
-                    if (p.legacy) {               // NumPy < 2: float32 scalar * int -> float64
-                        pc = ((double)a * p.ev_power) * p.ev_eff;
-                        change = (pc * p.dt) / cap;
-                    } else {                      // NumPy 2 (NEP 50): float32 product
-                        const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
-                        const float pdt = __fmul_rn(pf, p.dt_f);
-                        pc = (double)pf;
-                        change = (double)pdt / cap;
+                // penalise_charging_vehicles_outside_bounds (penaliser.py:39-57, 71-87): the vehicle's
+                // SoC and requested SoC at python index t-1; Python sum() order over the list.
+                if (t > 0 && (wj & W_PEN)) {
+                    const double req = p.req_stream ? s.req[(tbase + c) * (size_t)E + e] : 1.0;
+                    const double margin = 0.05 * req;
+                    if (r < req - margin) {
+                        const double d = (req - r) * 10;
+                        pen_v += d * d;
                     }
-                    const double calc = prev + change;
-                    if (a > 0.0f) {
-                        nsoc = (1.0 < calc) ? 1.0 : calc;                     // min(calc, 1.0)
-                        pw = pc;                                              // full power billed
+                }
+
+                // Charger.charge_or_discharge_vehicle (charger.py:37-56, 58-94, 108-144)
+                double pw = 0.0;
+                if (wj & W_OCC) {
+                    const double prev = (wj & W_STATIC) ? aux[j] : r;
+                    const double cap = (double)((wj >> W_CAP_SHIFT) & 0xffu);
+                    double nsoc = prev;
+                    if (a == 0.0f) {
+                        nsoc = prev;
+                    } else if (!p.bounded) {
+                        fl |= SNG_FLAG_CHARGING_MODE;
                     } else {
-                        pw = (calc >= 0.0) ? -((prev * cap) / p.dt) : pc;     // inverted flag, :122-132
-                        nsoc = (calc > 0.0) ? calc : 0.0;                     // max(0.0, calc)
+                        double pc, change;
+                        if (p.legacy) {               // NumPy < 2: float32 scalar * int -> float64
+                            pc = ((double)a * p.ev_power) * p.ev_eff;
+                            change = (pc * p.dt) / cap;
+                        } else {                      // NumPy 2 (NEP 50): float32 product
+                            const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
+                            const float pdt = __fmul_rn(pf, p.dt_f);
+                            pc = (double)pf;
+                            change = (double)pdt / cap;
+                        }
+                        const double calc = prev + change;
+                        if (a > 0.0f) {
+                            nsoc = (1.0 < calc) ? 1.0 : calc;                     // min(calc, 1.0)
+                            pw = pc;                                              // full power billed
+                        } else {
+                            pw = (calc >= 0.0) ? -((prev * cap) / p.dt) : pc;     // inverted flag, :122-132
+                            nsoc = (calc > 0.0) ? calc : 0.0;                     // max(0.0, calc)
+                        }
                     }
+                    r = nsoc;
+                } else {
+                    if (a != 0.0f) nonexist += 100.0;                             // reset_info_values, :146-156
+                    r = aux[j];                                                   // SOC[c, t] of an empty charger
                 }
-                run = nsoc;
-            } else {
-                if (a != 0.0f) nonexist += 100.0;                             // reset_info_values, :146-156
-                run = aux;                                                    // SOC[c, t] of an empty charger
-            }
-            s.soc[(size_t)c * E + e] = run;
-            if (pw > 0.0) pos.push(pw);
-            if (pw < 0.0) neg.push(pw);
+                socv[(size_t)c * E + e] = r;
+                if (pw > 0.0) pos.push(pw);
+                if (pw < 0.0) neg.push(pw);
 
-            o_row[k_soc + c] = (float)run;
-            o_row[k_dep + c] = (float)((double)((w >> W_DEP_SHIFT) & 0xffu) / 24);
+                o_row[k_soc + c] = (float)r;
+                o_row[k_dep + c] = (float)((double)((wj >> W_DEP_SHIFT) & 0xffu) / 24);
+            }
         }
         if (t == 0) pen_v = s.pen0[e];
 
@@ -259,20 +317,22 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
 
         if (fl) s.flags[e] |= fl;
         if (info.flags) info.flags[e] = fl;
-        if (info.grid_power) info.grid_power[e] = grid;
-        if (info.p_charge) info.p_charge[e] = p_ch;
-        if (info.p_discharge) info.p_discharge[e] = p_dis;
-        if (info.bess_soc) info.bess_soc[e] = p.bess ? bess : 0.0;
-        if (info.pen_vehicle) info.pen_vehicle[e] = pen_v;
-        if (info.pen_battery) info.pen_battery[e] = pen_b;
-        if (info.grid_cost) info.grid_cost[e] = cost;
-        if (info.total_cost) info.total_cost[e] = total;
-        if (info.solar) info.solar[e] = solar;
-        if (info.bess_power) info.bess_power[e] = bpow;
-        if (info.bess_calc_power) info.bess_calc_power[e] = bcalc;
-        if (info.nonexistent) info.nonexistent[e] = nonexist;
-        if (info.bess_initial) info.bess_initial[e] = p.bess ? s.bess0[e] : 0.0;
         if (info.episode_return) info.episode_return[e] += -total;
+        if (DIAG) {
+            if (info.grid_power) info.grid_power[e] = grid;
+            if (info.p_charge) info.p_charge[e] = p_ch;
+            if (info.p_discharge) info.p_discharge[e] = p_dis;
+            if (info.bess_soc) info.bess_soc[e] = p.bess ? bess : 0.0;
+            if (info.pen_vehicle) info.pen_vehicle[e] = pen_v;
+            if (info.pen_battery) info.pen_battery[e] = pen_b;
+            if (info.grid_cost) info.grid_cost[e] = cost;
+            if (info.total_cost) info.total_cost[e] = total;
+            if (info.solar) info.solar[e] = solar;
+            if (info.bess_power) info.bess_power[e] = bpow;
+            if (info.bess_calc_power) info.bess_calc_power[e] = bcalc;
+            if (info.nonexistent) info.nonexistent[e] = nonexist;
+            if (info.bess_initial) info.bess_initial[e] = p.bess ? s.bess0[e] : 0.0;
+        }
     }
     __syncthreads();
     copy_out(obs + e0 * O, s_obs, nblk * O, vec_io != 0, lane);
@@ -412,20 +472,38 @@ size_t step_lds_bytes(const Params &p) {
     return (((size_t)kWave * p.act_dim + 3) & ~(size_t)3) * 4 + (size_t)kWave * p.obs_dim * 4;
 }
 
+template <int NC, bool DIAG>
+static void launch_step_t(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
+                          double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream) {
+    const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
+    hipLaunchKernelGGL((step_kernel<NC, DIAG>), grid, block, step_lds_bytes(p), stream, p, s, info, act, obs, reward,
+                       done, E, t, vec_io);
+}
+
+template <bool DIAG>
+static void launch_step_n(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
+                          double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream) {
+    switch (p.n) {
+        case 1: launch_step_t<1, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+        case 2: launch_step_t<2, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+        case 4: launch_step_t<4, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+        case 8: launch_step_t<8, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+        case 10: launch_step_t<10, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+        case 16: launch_step_t<16, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+        case 50: launch_step_t<50, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+        default: launch_step_t<0, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+    }
+}
+
 hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
                        double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream) {
-    const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
-    const size_t lds = step_lds_bytes(p);
-    switch (p.n) {
-        case 1: hipLaunchKernelGGL(step_kernel<1>, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io); break;
-        case 2: hipLaunchKernelGGL(step_kernel<2>, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io); break;
-        case 4: hipLaunchKernelGGL(step_kernel<4>, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io); break;
-        case 8: hipLaunchKernelGGL(step_kernel<8>, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io); break;
-        case 10: hipLaunchKernelGGL(step_kernel<10>, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io); break;
-        case 16: hipLaunchKernelGGL(step_kernel<16>, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io); break;
-        case 50: hipLaunchKernelGGL(step_kernel<50>, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io); break;
-        default: hipLaunchKernelGGL(step_kernel<0>, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io); break;
-    }
+    const bool diag = info.grid_power || info.p_charge || info.p_discharge || info.bess_soc || info.pen_vehicle ||
+                      info.pen_battery || info.grid_cost || info.total_cost || info.solar || info.bess_power ||
+                      info.bess_calc_power || info.nonexistent || info.bess_initial;
+    if (diag)
+        launch_step_n<true>(p, s, info, act, obs, reward, done, E, t, vec_io, stream);
+    else
+        launch_step_n<false>(p, s, info, act, obs, reward, done, E, t, vec_io, stream);
     return hipGetLastError();
 }
 

@@ -335,7 +335,7 @@ class EpisodeGraph:
     """A whole day (device-RNG reset + T fused steps) captured once as a hipGraph and
     replayed; actions come from a device tensor [T, E, act_dim]."""
 
-    def __init__(self, venv, actions, with_reset=True):
+    def __init__(self, venv, actions, with_reset=True, timing=False):
         self.venv = venv
         self.actions = actions.contiguous()
         g = ctypes.c_void_p()
@@ -344,7 +344,7 @@ class EpisodeGraph:
                                          ctypes.c_void_p(venv.obs_d.data_ptr()),
                                          ctypes.c_void_p(venv.reward_d.data_ptr()),
                                          ctypes.c_void_p(venv.done_d.data_ptr()), ctypes.byref(venv._info),
-                                         int(with_reset), ctypes.byref(g)), venv._h)
+                                         int(with_reset) | (2 if timing else 0), ctypes.byref(g)), venv._h)
         self._g = g
 
     def launch(self, stream=None):
