@@ -10,8 +10,8 @@ exact zeros), pre-generated on the device outside the timed region.
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Rank 0 prints one JSON line.  `roofline` describes the dominant kernel (the fused step):
-achieved = algorithmic bytes per launch / mean launch time from HIP events captured around
-every step kernel in the graph (the last replay of the timed region); `traffic` comes from
+achieved = algorithmic bytes per launch / mean launch time from HIP start/stop events attached
+to every step-kernel dispatch (eager days right after the timed region); `traffic` comes from
 the committed rocprofv3 PMC summary (profiles/), null if absent.  `cpu_baseline` is the C
 oracle (a scalar port of the reference step/reset) on one host core, bounded sample.
 """
@@ -85,8 +85,7 @@ def main():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--graph-events", choices=["on", "off"], default="on",
-                    help="capture HIP events around every step kernel inside the timed graph")
+    ap.add_argument("--timing-days", type=int, default=3, help="eager days for the per-kernel HIP-event probe")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -116,7 +115,7 @@ def main():
     acts = acts.contiguous()
     # the bench's info: only the per-env day return (for the all-gather), no diagnostics
     venv._info.flags = None
-    graph = EpisodeGraph(venv, acts, with_reset=True, timing=args.graph_events == "on")
+    graph = EpisodeGraph(venv, acts, with_reset=True)
     gathered = torch.empty(world * E, dtype=torch.float64, device=device) if world > 1 else None
 
     def day():
@@ -138,20 +137,11 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    timing_src = "HIP events captured around every step kernel of the last timed replay"
-    try:
-        kernel_ms = graph.step_kernel_ms()
-    except Exception:
-        # eager pass with the same env/actions: HIP events around each step kernel on its stream
-        timing_src = "HIP events around each step kernel, eager day right after the timed region"
-        venv.reset_tensors(rng="device")
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(T)]
-        for t in range(T):
-            evs[t][0].record()
-            venv.step_tensors(acts[t])
-            evs[t][1].record()
-        torch.cuda.synchronize()
-        kernel_ms = np.array([a.elapsed_time(b) for a, b in evs])
+    # per-kernel device time: HIP start/stop events attached to every step-kernel dispatch
+    # (hipExtLaunchKernel) over eager days of the same env/actions, right after the timed region
+    kernel_ms = venv.time_step_kernels(acts, days=args.timing_days)
+    timing_src = (f"HIP start/stop events on each step-kernel dispatch (hipExtLaunchKernel), "
+                  f"{args.timing_days} eager days after the timed region, same stream/env/actions")
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -197,13 +197,14 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
  * holds T consecutive [num_envs][act_dim] blocks; obs/reward/done are overwritten every
  * step; info may be NULL.  Replays draw a new day each time.  flags: SNG_GRAPH_*. */
 #define SNG_GRAPH_RESET 1   /* start every replay with a device-RNG reset */
-#define SNG_GRAPH_TIMING 2  /* capture HIP events around every step kernel */
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
                      const SngInfo *info, int flags, SngGraph **out);
 int sng_graph_launch(SngGraph *graph, void *stream);
-/* Device time (ms) of each of the T step kernels in the most recent replay, measured by
- * HIP events captured around every step kernel in the graph.  Synchronises. */
-int sng_graph_step_times(SngGraph *graph, float *ms_per_step, int32_t n);
+/* Kernel-time probe: runs `days` device-RNG days eagerly (as the graph does) and returns the
+ * device time (ms) of every step kernel, ms[days*T], from HIP start/stop events attached to
+ * each dispatch (hipExtLaunchKernel: the dispatch's own begin/end timestamps).  Synchronises. */
+int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
+                          const SngInfo *info, int32_t days, float *ms, void *stream);
 void sng_graph_destroy(SngGraph *graph);
 
 /* Host-only entry points (no GPU needed): the reference-RNG scenario generator, for

@@ -20,7 +20,8 @@
 
 namespace sng {
 hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
-                       double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream);
+                       double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
+                       hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
                            int vec_io, hipStream_t stream);
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
@@ -345,7 +346,6 @@ struct SngGraph {
     SngEnv *env = nullptr;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
-    std::vector<hipEvent_t> ev;   // [2*T]: recorded around every step kernel of the day
 };
 
 namespace {
@@ -814,7 +814,7 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
                      const SngInfo *info, int flags, SngGraph **out) {
-    const bool with_reset = (flags & SNG_GRAPH_RESET) != 0, timing = (flags & SNG_GRAPH_TIMING) != 0;
+    const bool with_reset = (flags & SNG_GRAPH_RESET) != 0;
     if (!env || !actions || !obs || !reward || !done || !out) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     if (with_reset && env->i4 < 2) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
     HIP_TRY(env, hipSetDevice(env->device));
@@ -837,15 +837,8 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
         e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, cs);
         if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, cs);
     }
-    if (timing) g->ev.assign(2 * (size_t)p.T, nullptr);
-    for (auto &x : g->ev)
-        if (e == hipSuccess) e = hipEventCreate(&x);
-    for (int t = 0; e == hipSuccess && t < p.T; ++t) {
-        if (timing) e = hipEventRecordWithFlags(g->ev[2 * t], cs, hipEventRecordExternal);
-        if (e == hipSuccess)
-            e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
-        if (e == hipSuccess && timing) e = hipEventRecordWithFlags(g->ev[2 * t + 1], cs, hipEventRecordExternal);
-    }
+    for (int t = 0; e == hipSuccess && t < p.T; ++t)
+        e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
     hipGraph_t graph = nullptr;
     hipError_t e2 = hipStreamEndCapture(cs, &graph);
     if (e == hipSuccess) e = e2;
@@ -853,8 +846,6 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
     (void)hipStreamDestroy(cs);
     if (e != hipSuccess) {
         if (graph) (void)hipGraphDestroy(graph);
-        for (auto x : g->ev)
-            if (x) (void)hipEventDestroy(x);
         delete g;
         return hip_fail(env, e, "graph capture");
     }
@@ -878,21 +869,45 @@ void sng_graph_destroy(SngGraph *g) {
     (void)hipSetDevice(g->env->device);
     if (g->exec) (void)hipGraphExecDestroy(g->exec);
     if (g->graph) (void)hipGraphDestroy(g->graph);
-    for (auto x : g->ev)
-        if (x) (void)hipEventDestroy(x);
     delete g;
 }
 
-int sng_graph_step_times(SngGraph *g, float *ms, int32_t n) {
-    if (!g || !ms) return SNG_ERR_INVALID_ARGUMENT;
-    SngEnv *env = g->env;
+int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
+                          const SngInfo *info, int32_t days, float *ms, void *stream) {
+    if (!env || !actions || !obs || !reward || !done || !ms || days < 1)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    if (env->i4 < 2) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
     HIP_TRY(env, hipSetDevice(env->device));
-    const int T = (int)(g->ev.size() / 2);
-    if (T == 0) return fail(env, SNG_ERR_STATE, "graph was created without SNG_GRAPH_TIMING");
-    for (int t = 0; t < T && t < n; ++t) {
-        HIP_TRY(env, hipEventSynchronize(g->ev[2 * t + 1]));
-        HIP_TRY(env, hipEventElapsedTime(&ms[t], g->ev[2 * t], g->ev[2 * t + 1]));
+    hipStream_t st = (hipStream_t)stream;
+    Params p = env->p;
+    p.req_stream = p.req_enabled;
+    if (p.req_stream) {
+        int rc = ensure_req(env);
+        if (rc) return rc;
     }
+    const InfoPtrs ip = info_ptrs(info);
+    const int64_t E = env->E;
+    const int T = p.T, A = p.act_dim;
+    const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
+    std::vector<hipEvent_t> ev(2 * (size_t)T * days, nullptr);
+    hipError_t e = hipSuccess;
+    for (auto &x : ev)
+        if (e == hipSuccess) e = hipEventCreate(&x);
+    for (int d = 0; e == hipSuccess && d < days; ++d) {
+        e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, st);
+        if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, st);
+        for (int t = 0; e == hipSuccess && t < T; ++t) {
+            hipEvent_t a = ev[2 * ((size_t)d * T + t)], b = ev[2 * ((size_t)d * T + t) + 1];
+            e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, st, a, b);
+        }
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    for (int k = 0; e == hipSuccess && k < T * days; ++k) e = hipEventElapsedTime(&ms[k], ev[2 * k], ev[2 * k + 1]);
+    for (auto x : ev)
+        if (x) (void)hipEventDestroy(x);
+    if (e != hipSuccess) return hip_fail(env, e, "timed day");
+    env->t = T;
+    env->day_finished = true;
     return SNG_OK;
 }
 

@@ -11,6 +11,7 @@
 // the same order as the reference: numpy's pairwise sum for the charging powers
 // (charging_station.py:293-294) and Python's left-to-right sum() for penalties
 // (penaliser.py:55).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -472,38 +473,53 @@ size_t step_lds_bytes(const Params &p) {
     return (((size_t)kWave * p.act_dim + 3) & ~(size_t)3) * 4 + (size_t)kWave * p.obs_dim * 4;
 }
 
+// Optional start/stop events (ev != nullptr): hipExtLaunchKernel stamps them with the
+// dispatch's own begin/end timestamps, i.e. the kernel's device time.
+struct LaunchEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+};
+
 template <int NC, bool DIAG>
 static void launch_step_t(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
-                          double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream) {
+                          double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
+                          const LaunchEvents *ev) {
     const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
-    hipLaunchKernelGGL((step_kernel<NC, DIAG>), grid, block, step_lds_bytes(p), stream, p, s, info, act, obs, reward,
-                       done, E, t, vec_io);
+    if (ev)
+        hipExtLaunchKernelGGL((step_kernel<NC, DIAG>), grid, block, (uint32_t)step_lds_bytes(p), stream, ev->start,
+                              ev->stop, 0u, p, s, info, act, obs, reward, done, E, t, vec_io);
+    else
+        hipLaunchKernelGGL((step_kernel<NC, DIAG>), grid, block, step_lds_bytes(p), stream, p, s, info, act, obs,
+                           reward, done, E, t, vec_io);
 }
 
 template <bool DIAG>
 static void launch_step_n(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
-                          double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream) {
+                          double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
+                          const LaunchEvents *ev) {
     switch (p.n) {
-        case 1: launch_step_t<1, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
-        case 2: launch_step_t<2, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
-        case 4: launch_step_t<4, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
-        case 8: launch_step_t<8, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
-        case 10: launch_step_t<10, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
-        case 16: launch_step_t<16, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
-        case 50: launch_step_t<50, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
-        default: launch_step_t<0, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream); break;
+        case 1: launch_step_t<1, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 2: launch_step_t<2, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 4: launch_step_t<4, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 8: launch_step_t<8, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 10: launch_step_t<10, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 16: launch_step_t<16, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 50: launch_step_t<50, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        default: launch_step_t<0, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
     }
 }
 
 hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
-                       double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream) {
+                       double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
+                       hipEvent_t ev_start, hipEvent_t ev_stop) {
+    LaunchEvents evs{ev_start, ev_stop};
+    const LaunchEvents *ev = (ev_start && ev_stop) ? &evs : nullptr;
     const bool diag = info.grid_power || info.p_charge || info.p_discharge || info.bess_soc || info.pen_vehicle ||
                       info.pen_battery || info.grid_cost || info.total_cost || info.solar || info.bess_power ||
                       info.bess_calc_power || info.nonexistent || info.bess_initial;
     if (diag)
-        launch_step_n<true>(p, s, info, act, obs, reward, done, E, t, vec_io, stream);
+        launch_step_n<true>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev);
     else
-        launch_step_n<false>(p, s, info, act, obs, reward, done, E, t, vec_io, stream);
+        launch_step_n<false>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev);
     return hipGetLastError();
 }
 

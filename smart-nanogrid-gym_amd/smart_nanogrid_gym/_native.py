@@ -113,7 +113,9 @@ EXPORTS = {
                                         ctypes.POINTER(ctypes.c_void_p)]),
     "sng_graph_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "sng_graph_destroy": (None, [ctypes.c_void_p]),
-    "sng_graph_step_times": (ctypes.c_int, [ctypes.c_void_p, c_float_p, ctypes.c_int32]),
+    "sng_time_step_kernels": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.POINTER(SngInfo), ctypes.c_int32, c_float_p,
+                                             ctypes.c_void_p]),
     "sng_host_generate_scenarios": (ctypes.c_int, [ctypes.POINTER(SngConfig), ctypes.c_int64, ctypes.c_uint64,
                                                    ctypes.c_int32, c_double_p, c_double_p, c_double_p, c_double_p,
                                                    c_int32_p, c_int32_p, ctypes.c_int32, c_double_p]),

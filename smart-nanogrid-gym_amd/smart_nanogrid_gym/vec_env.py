@@ -318,6 +318,19 @@ class SmartNanogridVecEnv:
         check(lib().sng_get_vehicle_soc(self._h, out.ctypes.data_as(_native.c_double_p)), self._h)
         return out
 
+    def time_step_kernels(self, actions, days=1):
+        """Device time (ms) of every step kernel over `days` eager device-RNG days, from HIP
+        start/stop events attached to each kernel dispatch; actions [T, E, act_dim] on the device."""
+        a = actions.contiguous()
+        out = np.zeros(days * self.timesteps, np.float32)
+        with torch.cuda.device(self.device):
+            check(lib().sng_time_step_kernels(self._h, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(self.obs_d.data_ptr()),
+                                              ctypes.c_void_p(self.reward_d.data_ptr()),
+                                              ctypes.c_void_p(self.done_d.data_ptr()), ctypes.byref(self._info),
+                                              days, out.ctypes.data_as(_native.c_float_p),
+                                              _stream_handle(self.device)), self._h)
+        return out
+
     def tables(self):
         n = ctypes.c_int32()
         irr = np.zeros(512)
@@ -335,7 +348,7 @@ class EpisodeGraph:
     """A whole day (device-RNG reset + T fused steps) captured once as a hipGraph and
     replayed; actions come from a device tensor [T, E, act_dim]."""
 
-    def __init__(self, venv, actions, with_reset=True, timing=False):
+    def __init__(self, venv, actions, with_reset=True):
         self.venv = venv
         self.actions = actions.contiguous()
         g = ctypes.c_void_p()
@@ -344,18 +357,12 @@ class EpisodeGraph:
                                          ctypes.c_void_p(venv.obs_d.data_ptr()),
                                          ctypes.c_void_p(venv.reward_d.data_ptr()),
                                          ctypes.c_void_p(venv.done_d.data_ptr()), ctypes.byref(venv._info),
-                                         int(with_reset) | (2 if timing else 0), ctypes.byref(g)), venv._h)
+                                         int(with_reset), ctypes.byref(g)), venv._h)
         self._g = g
 
     def launch(self, stream=None):
         s = _stream_handle(self.venv.device) if stream is None else ctypes.c_void_p(stream)
         check(lib().sng_graph_launch(self._g, s), self.venv._h)
-
-    def step_kernel_ms(self):
-        """Device time of each step kernel in the latest replay (HIP events inside the graph)."""
-        out = np.zeros(self.venv.timesteps, np.float32)
-        check(lib().sng_graph_step_times(self._g, out.ctypes.data_as(_native.c_float_p), out.size), self.venv._h)
-        return out
 
     def close(self):
         if getattr(self, "_g", None):
