@@ -1,0 +1,62 @@
+"""Summarise rocprofv3 runs of bench.py into profiles/.
+
+  python tools/pmc_summary.py <round-tag> [gpurun_out]
+
+Reads <out>/prof/run_kernel_stats.csv (--kernel-trace --stats) and the two PMC passes
+<out>/pmc_fetch/run_counter_collection.csv (FETCH_SIZE) and <out>/pmc_write/... (WRITE_SIZE),
+writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.csv and profiles/pmc_step_kernel.json.
+
+HBM bytes per launch (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
+on gfx950 FETCH_SIZE counts half the bytes of a coalesced streaming read, so
+traffic = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024.  The 2x was checked against this kernel's
+own known read volume (the bench's algorithmic read bytes / raw FETCH_SIZE = 1.96).
+"""
+import collections
+import csv
+import json
+import os
+import shutil
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def per_kernel(path, counter):
+    agg = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter:
+            agg[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in agg.items()}, {k: len(v) for k, v in agg.items()}
+
+
+def main():
+    tag = sys.argv[1]
+    out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out")
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copyfile(os.path.join(out, "prof", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    fetch, nf = per_kernel(os.path.join(out, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+    write, nw = per_kernel(os.path.join(out, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+    rows = []
+    for k in sorted(set(fetch) | set(write)):
+        if "sng::" not in k:
+            continue
+        f, w = fetch.get(k, 0.0), write.get(k, 0.0)
+        rows.append(dict(kernel=k.split("(")[0], dispatches=nf.get(k, 0), fetch_kib=round(f, 1), write_kib=round(w, 1),
+                         hbm_bytes_per_launch=int(2 * f * 1024 + w * 1024)))
+    with open(os.path.join(prof, f"{tag}_pmc.csv"), "w", newline="") as fp:
+        wr = csv.DictWriter(fp, fieldnames=list(rows[0]))
+        wr.writeheader()
+        wr.writerows(rows)
+    step = [r for r in rows if "step_kernel" in r["kernel"]][0]
+    meta = dict(source=f"profiles/{tag}_pmc.csv (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes)",
+                kernel=step["kernel"], envs=65536, chargers=10, bytes_per_launch=step["hbm_bytes_per_launch"],
+                fetch_kib=step["fetch_kib"], write_kib=step["write_kib"],
+                correction="traffic = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts half of streamed reads)")
+    json.dump(meta, open(os.path.join(prof, "pmc_step_kernel.json"), "w"), indent=1)
+    for r in rows:
+        print(r)
+
+
+if __name__ == "__main__":
+    main()
