@@ -165,6 +165,12 @@ const char *sng_last_error(const SngEnv *env);
 int sng_get_dims(const SngEnv *env, SngDims *out);
 int sng_get_timestep(const SngEnv *env);
 
+/* Global index of this handle's env 0 when one population of envs is sharded over several
+ * GPUs/processes: env i then draws the streams of global env offset+i (reference RNG:
+ * seed + offset + i; device RNG: Philox counter offset + i), so a sharded run reproduces the
+ * single-GPU run bit for bit.  Call before reset. */
+int sng_set_env_offset(SngEnv *env, int64_t offset);
+
 /* SmartNanogridEnv.reset() (smart_nanogrid_environment.py:320-360): new day for every
  * env, timestep 0, writes the t=0 observation into obs[num_envs][obs_dim]. */
 int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream);

@@ -639,6 +639,15 @@ int sng_get_dims(const SngEnv *env, SngDims *out) {
 
 int sng_get_timestep(const SngEnv *env) { return env ? env->t : -1; }
 
+int sng_set_env_offset(SngEnv *env, int64_t offset) {
+    if (!env || offset < 0) return fail(env, SNG_ERR_INVALID_ARGUMENT, "bad env offset");
+    env->p.env_offset = offset;
+    env->np_rng.clear();   // reference streams are re-seeded (seed + offset + i) at the next reset
+    env->py_rng.clear();
+    env->day_finished = false;
+    return SNG_OK;
+}
+
 int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     if (!env || !obs) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     HIP_TRY(env, hipSetDevice(env->device));
@@ -664,8 +673,9 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
         env->np_rng.resize(env->E);
         env->py_rng.resize(env->E);
         for (int64_t i = 0; i < env->E; ++i) {
-            env->np_rng[i].seed_numpy((uint32_t)(env->seed + (uint64_t)i));
-            env->py_rng[i].seed_python(env->seed + (uint64_t)i);
+            const uint64_t s = env->seed + (uint64_t)env->p.env_offset + (uint64_t)i;
+            env->np_rng[i].seed_numpy((uint32_t)s);
+            env->py_rng[i].seed_python(s);
         }
     }
     const bool with_req = env->p.req_enabled != 0;

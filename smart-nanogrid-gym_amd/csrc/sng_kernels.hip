@@ -408,7 +408,7 @@ __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s
     if (e >= E) return;
     const uint64_t day = *s.episode;
     const Philox rng{(uint32_t)seed, (uint32_t)(seed >> 32)};
-    const uint32_t ce = (uint32_t)e, cday = (uint32_t)day;
+    const uint32_t ce = (uint32_t)(e + p.env_offset), cday = (uint32_t)day;   // global env id
     uint32_t draw = 0;
     const int T = p.T, n = p.n;
 

@@ -72,6 +72,7 @@ struct Params {
     double ev_power, ev_eff;
     double bess_cap, bess_pmax_ch, bess_pmax_dis, bess_eff_ch, bess_eff_dis, bess_dod;
     double grid_w, bat_pen_w, sell_coef;
+    int64_t env_offset;       // global index of env 0 of this handle (sharded runs)
 };
 
 struct DeviceState {

@@ -96,6 +96,7 @@ EXPORTS = {
     "sng_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
     "sng_get_dims": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SngDims)]),
     "sng_get_timestep": (ctypes.c_int, [ctypes.c_void_p]),
+    "sng_set_env_offset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "sng_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "sng_reset_from_scenario": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SngScenario), ctypes.c_void_p,
                                                ctypes.c_void_p]),

@@ -42,11 +42,13 @@ class SmartNanogridVecEnv:
       device -- HIP device index
       rng    -- 'reference' (host MT19937 streams, reference-exact days) or 'device' (Philox on the GPU)
       info   -- True: also fill the per-step diagnostics (grid power, BESS SoC, penalties ...)
+      env_offset -- global index of env 0 when one env population is sharded over GPUs
+                    (parallel.shard_envs); env i then behaves as global env env_offset + i
     """
 
     metadata = {"render_modes": []}
 
-    def __init__(self, num_envs=1, *, seed=0, device=0, rng="reference", info=False, **env_kwargs):
+    def __init__(self, num_envs=1, *, seed=0, device=0, rng="reference", info=False, env_offset=0, **env_kwargs):
         if torch is None or not torch.cuda.is_available():
             raise RuntimeError("SmartNanogridVecEnv needs a HIP device (torch.cuda unavailable)")
         self.settings = EnvSettings(**env_kwargs)
@@ -59,6 +61,9 @@ class SmartNanogridVecEnv:
         h = ctypes.c_void_p()
         check(lib().sng_create(ctypes.byref(cfg), device, self.num_envs, self._seed, ctypes.byref(h)))
         self._h = h
+        self.env_offset = int(env_offset)
+        if self.env_offset:
+            check(lib().sng_set_env_offset(h, self.env_offset), h)
         dims = _native.SngDims()
         check(lib().sng_get_dims(h, ctypes.byref(dims)), h)
         self.obs_dim, self.act_dim, self.timesteps = dims.obs_dim, dims.act_dim, dims.timesteps

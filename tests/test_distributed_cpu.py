@@ -1,0 +1,83 @@
+"""The N>1 path on CPU: world_size-2 gloo, env sharding by global index and the per-day
+all-gather of returns.  The per-rank env simulation is the oracle here (the GPU envs are
+covered by the gpu-marked sharding test); what this checks is the sharding arithmetic and
+the collective: the gathered returns equal one process simulating the whole population."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle as O
+from smart_nanogrid_gym.parallel import all_gather_returns, day_summary, max_over_ranks, shard_envs
+
+KW = dict(number_of_chargers=4, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+TOTAL, SEED = 48, 321
+
+
+def day_returns(global_ids):
+    cfg = O.OracleConfig(**KW)
+    out = []
+    for g in global_ids:
+        env = O.OracleEnv(cfg, SEED + int(g))
+        env.reset()
+        rng = np.random.default_rng(int(g))
+        total = 0.0
+        for t in range(cfg.T):
+            a = rng.uniform(0, 1, cfg.act_dim).astype(np.float32)
+            a[-1] = a[-1] * 2 - 1
+            total += env.step(a)[1]
+        out.append(total)
+    return np.array(out)
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, cnt = shard_envs(TOTAL, world, rank)
+    local = torch.from_numpy(day_returns(range(off, off + cnt)))
+    gathered = all_gather_returns(local)
+    slowest = max_over_ranks(float(rank + 1))
+    if rank == 0:
+        q.put((gathered.numpy(), slowest, day_summary(gathered)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_shard_envs_covers_population():
+    for total, world in [(10, 3), (65536 * 8, 8), (7, 7), (100, 1)]:
+        ranges = [shard_envs(total, world, r) for r in range(world)]
+        assert ranges[0][0] == 0
+        for (o1, c1), (o2, _) in zip(ranges, ranges[1:]):
+            assert o1 + c1 == o2
+        assert sum(c for _, c in ranges) == total
+    with pytest.raises(ValueError):
+        shard_envs(2, 4, 0)
+
+
+def test_gloo_world2_gather_matches_single_process():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered, slowest, summary = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(gathered, day_returns(range(TOTAL)))
+    assert slowest == 2.0
+    assert summary["envs"] == TOTAL and summary["max_return"] <= 0

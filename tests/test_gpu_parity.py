@@ -262,3 +262,28 @@ def test_reference_errors_are_raised():
     with pytest.raises(ValueError, match="penalty mode"):
         env.reset()
     env.close()
+
+
+@pytest.mark.parametrize("rng", ["device", "reference"])
+def test_sharded_population_reproduces_single_gpu(rng):
+    """Two handles with env_offset 0 / E/2 (what each rank of a 2-GPU run holds) give the same
+    days, rewards and returns as one handle over all E envs."""
+    E, N = 2048, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    full = SmartNanogridVecEnv(E, seed=5, rng=rng, **kw)
+    halves = [SmartNanogridVecEnv(E // 2, seed=5, rng=rng, env_offset=k * (E // 2), **kw) for k in range(2)]
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    for day in range(2):
+        o_full = full.reset_tensors().clone()
+        o_half = torch.cat([h.reset_tensors().clone() for h in halves])
+        assert torch.equal(o_full, o_half)
+        for t in range(24):
+            of, rf, _ = full.step_tensors(acts[t])
+            parts = [h.step_tensors(acts[t, k * (E // 2):(k + 1) * (E // 2)].contiguous()) for k, h in enumerate(halves)]
+            assert torch.equal(of, torch.cat([p[0] for p in parts]))
+            assert torch.equal(rf, torch.cat([p[1] for p in parts]))
+        assert torch.equal(full.return_d, torch.cat([h.return_d for h in halves]))
+    for v in [full] + halves:
+        v.close()
