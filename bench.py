@@ -82,6 +82,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--chargers", type=int, default=10)
+    ap.add_argument("--lanes", type=int, default=0, help="step kernel lanes per env (0 = library default)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -100,12 +101,15 @@ def main():
     torch.cuda.set_device(device)
 
     from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv
+    from smart_nanogrid_gym.parallel import max_over_ranks, shard_envs
 
     E, N = args.envs, args.chargers
     kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
               vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
               battery_system_available_in_model=True)
-    venv = SmartNanogridVecEnv(E, seed=args.seed + rank * E, device=local, rng="device", **kw)
+    offset, _ = shard_envs(world * E, world, rank)   # weak scaling: E envs per GPU, global ids
+    venv = SmartNanogridVecEnv(E, seed=args.seed, device=local, rng="device", env_offset=offset,
+                               step_lanes_per_env=args.lanes, **kw)
     T, A = venv.timesteps, venv.act_dim
     g = torch.Generator(device=device).manual_seed(args.seed + rank)
     low = torch.tensor(venv.action_space.low, device=device)
@@ -142,10 +146,7 @@ def main():
     kernel_ms = venv.time_step_kernels(acts, days=args.timing_days)
     timing_src = (f"HIP start/stop events on each step-kernel dispatch (hipExtLaunchKernel), "
                   f"{args.timing_days} eager days after the timed region, same stream/env/actions")
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, device=device)
     # sanity: a day's returns are finite and <= 0
     ret = venv.return_d.cpu().numpy()
     assert np.isfinite(ret).all() and (ret <= 0).all()

@@ -100,6 +100,8 @@ typedef struct SngConfig {
     /* PV input: per-minute irradiance (W/m^2), solar_irradiance.mat['irradiance'] */
     const double *irradiance_per_minute;
     int64_t irradiance_minutes;
+    /* Kernel tuning: GPU lanes per environment in the step kernel (0 = automatic; 1, 2, 4). */
+    int32_t step_lanes_per_env;
 } SngConfig;
 
 typedef struct SngDims {

@@ -26,6 +26,7 @@ hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, do
                            int vec_io, hipStream_t stream);
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            hipStream_t stream);
+int step_lanes_supported(int n, int lanes);
 }  // namespace sng
 
 using namespace sng;
@@ -547,6 +548,15 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
     p.grid_w = c.grid_cost_weight;
     p.bat_pen_w = c.battery_penalty_weight;
     p.sell_coef = c.selling_price_coefficient;
+    if (c.step_lanes_per_env) {
+        if (!step_lanes_supported(p.n, c.step_lanes_per_env)) {
+            delete env;
+            return fail(nullptr, SNG_ERR_UNSUPPORTED, "step_lanes_per_env not available for this charger count");
+        }
+        p.lanes = c.step_lanes_per_env;
+    } else {
+        p.lanes = step_lanes_supported(p.n, 2) ? 2 : 1;   // tuned on MI355X at N=10, E=65,536
+    }
     env->i4 = (int)(4 / p.dt);
     env->i10 = (int)(10 / p.dt);
     env->i1 = (int)(1 / p.dt);

@@ -1,22 +1,26 @@
 // sng_kernels.hip -- HIP kernels of the batched SmartNanogridEnv hot path (gfx950).
 //
-// One thread = one environment; one 64-thread workgroup = one wavefront = 64 envs.
-// Per-env state is SoA with the env index fastest (sng_layout.h), so every per-charger
-// load/store of a wavefront is one contiguous 256 B (u32) or 512 B (f64) run.
-// The policy-facing row-major actions [E][A] and observations [E][O] are staged
-// through LDS so the HBM side of both is a contiguous, 16-byte-per-lane stream.
+// Step kernel mapping: L lanes per environment (L = 1, 2 or 4), 64/L environments per
+// 64-thread workgroup (one wavefront).  Lane `part` of an env owns a contiguous range of
+// chargers; the env's first lane (the leader) finishes the env (sums, BESS, cost, reward).
+// With L > 1 a 65,536-env step runs 2048-4096 wavefronts instead of 1024, which is what
+// keeps enough HBM requests in flight on 256 CUs.
 //
-// Arithmetic follows the reference operation for operation (no FMA contraction:
-// built with -ffp-contract=off); see the per-line citations.  Sums over chargers use
-// the same order as the reference: numpy's pairwise sum for the charging powers
-// (charging_station.py:293-294) and Python's left-to-right sum() for penalties
-// (penaliser.py:55).
+// Per-env state is SoA with the env index fastest (sng_layout.h), so every per-charger
+// load/store of a wavefront is a contiguous run.  The policy-facing row-major actions
+// [E][A] and observations [E][O] are staged through LDS so their HBM side is a contiguous,
+// 16-byte-per-lane stream.
+//
+// Arithmetic follows the reference operation for operation (built with -ffp-contract=off).
+// Sums over chargers use the reference's order: numpy's pairwise sum for the charging
+// powers (charging_station.py:293-294) and Python's left-to-right sum() for the vehicle
+// penalties (penaliser.py:55).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "sng_layout.h"
 #include "sng.h"
+#include "sng_layout.h"
 
 namespace sng {
 
@@ -33,7 +37,10 @@ struct PairwiseSum {
     int n;
     __device__ __forceinline__ void init() {
 #pragma unroll
-        for (int q = 0; q < 8; ++q) { r[q] = 0.0; b[q] = 0.0; }
+        for (int q = 0; q < 8; ++q) {
+            r[q] = 0.0;
+            b[q] = 0.0;
+        }
         n = 0;
     }
     __device__ __forceinline__ void push(double x) {
@@ -57,14 +64,11 @@ struct PairwiseSum {
     }
 };
 
-__device__ __forceinline__ size_t lds_obs_offset(int act_dim) {
-    // obs staging area starts after the actions, rounded to 16 bytes
-    return ((size_t)kWave * act_dim + 3) & ~(size_t)3;
-}
+__host__ __device__ constexpr int round4(int x) { return (x + 3) & ~3; }
 
 // Copy `count` floats global -> LDS with 16 B per lane when the run is aligned.  Each lane
-// issues up to K loads before the first LDS write, so the whole copy is one HBM round trip
-// when count <= K * 256 floats.
+// issues up to K loads before the first LDS write (clamped, unconditional loads: no per-element
+// branch + wait), so the whole copy is one HBM round trip when count <= K * 256 floats.
 template <int K>
 __device__ __forceinline__ void copy_in(float *__restrict__ dst, const float *__restrict__ src, int count,
                                         bool vec, int lane) {
@@ -75,7 +79,7 @@ __device__ __forceinline__ void copy_in(float *__restrict__ dst, const float *__
         for (int base = 0; base < n4; base += K * kWave) {
             float4 v[K];
 #pragma unroll
-            for (int k = 0; k < K; ++k) {   // clamped, unconditional: no per-element branch + wait
+            for (int k = 0; k < K; ++k) {
                 const int i = base + k * kWave + lane;
                 v[k] = s4[i < n4 ? i : n4 - 1];
             }
@@ -115,7 +119,7 @@ __device__ __forceinline__ void copy_out(float *__restrict__ dst, const float *_
 
 // Observation header (smart_nanogrid_environment.py:199-240, central_management_system.py:53-60):
 // [solar(t), price(t), solar(t+1..t+3), price(t+1..t+3)] with PV, [price(t), price(t+1..t+3)] without.
-__device__ __forceinline__ int write_obs_header(float *o, const Params &p, const Tables *tb, int t, double ratio) {
+__device__ __forceinline__ void write_obs_header(float *o, const Params &p, const Tables *tb, int t, double ratio) {
     int k = 0;
     if (p.pv) o[k++] = (float)(tb->irr_norm[t] * ratio);
     o[k++] = (float)tb->price_norm[t];
@@ -125,37 +129,205 @@ __device__ __forceinline__ int write_obs_header(float *o, const Params &p, const
     }
 #pragma unroll
     for (int j = 1; j <= 3; ++j) o[k++] = (float)tb->price_norm[t + j];
-    return k;
+}
+
+// Remaining time to departure / 24 (smart_nanogrid_environment.py:216-217) as float32.
+// (float)((double)d / 24) equals the correctly rounded float32 quotient for every integer d < 256
+// (d/24 is never a float32 rounding midpoint), so the cheaper float32 division is exact here.
+__device__ __forceinline__ float departure_obs(uint32_t w) {
+    return (float)((w >> W_DEP_SHIFT) & 0xffu) / 24.0f;
 }
 
 // ---------------------------------------------------------------------------------
-// The fused step: SmartNanogridEnv.step(actions) for 64 envs per workgroup.
-// NC   = compile-time charger count (0: runtime p.n);
-// DIAG = also write the per-step diagnostics (SngInfo arrays).
-// All per-charger loads of a batch of CH chargers are issued before any of them is used
-// (and the first batch before the action staging wait), so a wavefront keeps
-// 3*CH + 2 independent HBM requests in flight instead of one round trip per charger.
+// One charger, one step: penalty term of the vehicle present at t-1 and the EV update.
+// penalise_charging_vehicles_outside_bounds (penaliser.py:39-57, 71-87): SoC and requested
+// SoC at python index t-1.  Charger.charge_or_discharge_vehicle (charger.py:37-56, 58-94,
+// 108-144) and reset_info_values (:146-156).
 // ---------------------------------------------------------------------------------
-template <int NC, bool DIAG>
+struct ChargerResult {
+    double pw;      // charger power value (kW), f64 array element of charging_station.py:282
+    double q;       // insufficient-charge penalty term (0 if not checked / not insufficient)
+    double soc;     // SOC[c, t] after the step
+    double nonexist;
+    uint32_t fl;
+};
+
+__device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, float a,
+                                                      int t, const double *__restrict__ req_ptr) {
+    ChargerResult o{0.0, 0.0, run, 0.0, 0u};
+    if (t > 0 && (w & W_PEN)) {
+        const double req = p.req_stream ? *req_ptr : 1.0;
+        const double margin = 0.05 * req;
+        if (run < req - margin) {
+            const double d = (req - run) * 10;
+            o.q = d * d;
+        }
+    }
+    if (w & W_OCC) {
+        const double prev = (w & W_STATIC) ? aux : run;
+        const double cap = (double)((w >> W_CAP_SHIFT) & 0xffu);
+        double nsoc = prev;
+        if (a == 0.0f) {
+            nsoc = prev;
+        } else if (!p.bounded) {
+            o.fl |= SNG_FLAG_CHARGING_MODE;
+        } else {
+            double pc, change;
+            if (p.legacy) {   // NumPy < 2: float32 scalar * int -> float64
+                pc = ((double)a * p.ev_power) * p.ev_eff;
+                change = (pc * p.dt) / cap;
+            } else {          // NumPy 2 (NEP 50): float32 product
+                const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
+                const float pdt = __fmul_rn(pf, p.dt_f);
+                pc = (double)pf;
+                change = (double)pdt / cap;
+            }
+            const double calc = prev + change;
+            if (a > 0.0f) {
+                nsoc = (1.0 < calc) ? 1.0 : calc;                     // min(calc, 1.0)
+                o.pw = pc;                                            // full power billed
+            } else {
+                o.pw = (calc >= 0.0) ? -((prev * cap) / p.dt) : pc;   // inverted flag, :122-132
+                nsoc = (calc > 0.0) ? calc : 0.0;                     // max(0.0, calc)
+            }
+        }
+        o.soc = nsoc;
+    } else {
+        if (a != 0.0f) o.nonexist = 100.0;
+        o.soc = aux;   // SOC[c, t] of an empty charger
+    }
+    return o;
+}
+
+// ---------------------------------------------------------------------------------
+// Env tail: BESS, grid energy, cost, reward (central_management_system.py:99-185,
+// battery_energy_storage_system.py:186-262, penaliser.py:104-111/177-187,
+// accountant.py:213-227) and the observation header.  Leader lane only.
+// ---------------------------------------------------------------------------------
+template <bool DIAG>
+__device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, const InfoPtrs &info, int64_t e,
+                                         int t, double ratio, double bess, float bess_action, double p_ch,
+                                         double p_dis, double pen_v, double nonexist, uint32_t fl, float *o_row,
+                                         double *__restrict__ reward, uint8_t *__restrict__ done) {
+    const Tables *tb = s.tables;
+    const double solar = p.pv ? tb->pv_power[t] * ratio : 0.0;   // central_management_system.py:99-103
+    const double demand = p_ch + p_dis;                            // :105
+    if (demand < 0.0) fl |= p.v2x ? SNG_FLAG_V2X_BREAKPOINT : SNG_FLAG_NEGATIVE_DEMAND;
+    double rem = demand - solar;                                   // :167
+
+    double pen_b = 0.0, bpow = 0.0, bcalc = 0.0;
+    if (p.bess) {
+        if (t == 0) s.bess0[e] = bess;                             // :93-94
+        const double ba = (double)bess_action;
+        if (ba == 0.0) {
+            bpow = 0.0;
+            bcalc = 0.0;
+        } else if (!p.bounded) {
+            fl |= SNG_FLAG_CHARGING_MODE;
+        } else if (ba > 0.0) {
+            const double avail = -rem;
+            const double cp = (ba * p.bess_pmax_ch) * p.bess_eff_ch;
+            const double calc = bess + (cp * p.dt) / p.bess_cap;
+            bcalc = cp;
+            bess = (1.0 < calc) ? 1.0 : calc;
+            bpow = cp;
+            rem = -(avail - cp);
+        } else {
+            double dp = (ba * p.bess_pmax_dis) * p.bess_eff_dis;
+            const double calc = bess + (dp * p.dt) / p.bess_cap;
+            bcalc = dp;
+            if (calc < 0.0) dp = -((bess * p.bess_cap) / p.dt);
+            bess = (calc > 0.0) ? calc : 0.0;
+            bpow = dp;
+            rem = rem + dp;
+        }
+        if (bess < p.bess_dod) {                                   // penaliser.py:104-111
+            const double d = (p.bess_dod - bess) * 10;
+            pen_b = d * d;
+        } else if (!(bess <= 1.0)) {
+            fl |= SNG_FLAG_BESS_SOC_ABOVE_1;
+        }
+        s.bess[e] = bess;
+    }
+
+    const double grid = rem;
+    const double energy = grid * p.dt;
+    const double price = tb->price[t];
+    const double cost = (energy < 0.0) ? (energy * p.sell_coef) * price : energy * price;
+    const double tot_pen = p.bat_pen_w * pen_b + pen_v;
+    const double total = p.grid_w * fabs(cost) + tot_pen;
+    reward[e] = -total;
+    done[e] = (t + 1 == p.T) ? 1 : 0;
+
+    write_obs_header(o_row, p, tb, t, ratio);
+    if (p.bess) o_row[p.obs_dim - 1] = (float)bess;
+
+    if (fl) s.flags[e] |= fl;
+    if (info.flags) info.flags[e] = fl;
+    if (info.episode_return) info.episode_return[e] += -total;
+    if (DIAG) {
+        if (info.grid_power) info.grid_power[e] = grid;
+        if (info.p_charge) info.p_charge[e] = p_ch;
+        if (info.p_discharge) info.p_discharge[e] = p_dis;
+        if (info.bess_soc) info.bess_soc[e] = p.bess ? bess : 0.0;
+        if (info.pen_vehicle) info.pen_vehicle[e] = pen_v;
+        if (info.pen_battery) info.pen_battery[e] = pen_b;
+        if (info.grid_cost) info.grid_cost[e] = cost;
+        if (info.total_cost) info.total_cost[e] = total;
+        if (info.solar) info.solar[e] = solar;
+        if (info.bess_power) info.bess_power[e] = bpow;
+        if (info.bess_calc_power) info.bess_calc_power[e] = bcalc;
+        if (info.nonexistent) info.nonexistent[e] = nonexist;
+        if (info.bess_initial) info.bess_initial[e] = p.bess ? s.bess0[e] : 0.0;
+    }
+}
+
+// LDS layout of the step kernel for ENVS envs per workgroup.
+template <int L>
+struct StepLds {
+    __host__ __device__ static int act_floats(int envs, int A) { return round4(envs * A); }
+    __host__ __device__ static int obs_floats(int envs, int O) { return round4(envs * O); }
+    __host__ __device__ static size_t bytes(int envs, int A, int O, int n) {
+        return (size_t)(act_floats(envs, A) + obs_floats(envs, O)) * 4 + (L > 1 ? (size_t)2 * envs * n * 8 : 0);
+    }
+};
+
+// ---------------------------------------------------------------------------------
+// The fused step: SmartNanogridEnv.step(actions) for 64/L envs per workgroup.
+// NC   = compile-time charger count (0: runtime p.n, L must be 1);
+// L    = lanes per env;
+// DIAG = also write the per-step diagnostics (SngInfo arrays).
+// Every per-charger load of a lane's batch is issued before any of it is used, and the first
+// batch before the action staging wait, so one lane keeps 3*CH + 2 requests in flight.
+// ---------------------------------------------------------------------------------
+template <int NC, int L, bool DIAG>
 __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, InfoPtrs info,
                                                      const float *__restrict__ act, float *__restrict__ obs,
                                                      double *__restrict__ reward, uint8_t *__restrict__ done,
                                                      int64_t E, int t, int vec_io) {
-    constexpr int CH = (NC > 0 && NC <= 16) ? NC : 8;
+    static_assert(L == 1 || NC > 0, "multi-lane envs need a compile-time charger count");
+    constexpr int ENVS = kWave / L;
+    constexpr int CH = (L > 1) ? (NC + L - 1) / L : ((NC > 0 && NC <= 16) ? NC : 8);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int n = NC ? NC : p.n;
     const int A = p.act_dim, O = p.obs_dim;
     const int lane = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * kWave;
-    const int nblk = (int)((E - e0) < kWave ? (E - e0) : kWave);
-    const int64_t e = e0 + lane;
-    const bool live = lane < nblk;
+    const int le = lane / L, part = lane % L;
+    const int64_t e0 = (int64_t)blockIdx.x * ENVS;
+    const int nblk = (int)((E - e0) < ENVS ? (E - e0) : ENVS);
+    const int64_t e = e0 + le;
+    const bool live = le < nblk;
+    const bool leader = part == 0;
     float *s_act = lds;
-    float *s_obs = lds + lds_obs_offset(A);
+    float *s_obs = lds + StepLds<L>::act_floats(ENVS, A);
+    double *s_pw = reinterpret_cast<double *>(s_obs + StepLds<L>::obs_floats(ENVS, O));   // [ENVS][n], L > 1
+    double *s_q = s_pw + ENVS * n;
     const uint32_t *__restrict__ word = s.word;
     const double *__restrict__ auxv = s.aux;
     double *__restrict__ socv = s.soc;
     const size_t tbase = (size_t)t * n;
+    const int cbeg = (L > 1) ? part * CH : 0;
+    const int cend = (L > 1) ? ((cbeg + CH) < n ? (cbeg + CH) : n) : n;
 
     uint32_t w[CH];
     double aux[CH], run[CH];
@@ -163,7 +335,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int c = c0 + j;
-            if (c < n) {
+            if (c < cend) {
                 const size_t idx = (tbase + c) * (size_t)E + e;
                 w[j] = word[idx];
                 aux[j] = auxv[idx];
@@ -174,166 +346,70 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
 
     double ratio = 0.0, bess = 0.0;
     if (live) {
-        ratio = s.ratio[e];
-        if (p.bess) bess = s.bess[e];
-        load_batch(0);
+        if (leader) {
+            ratio = s.ratio[e];
+            if (p.bess) bess = s.bess[e];
+        }
+        load_batch(cbeg);
     }
     copy_in<(NC > 0 && NC < 16) ? 4 : 8>(s_act, act + e0 * A, nblk * A, vec_io != 0, lane);
     __syncthreads();
 
+    const float *a_row = s_act + le * A;
+    float *o_row = s_obs + le * O;
+    const int k_soc = (p.pv ? 8 : 4);
+    PairwiseSum pos, neg;
+    pos.init();
+    neg.init();
+    double pen_v = 0.0, nonexist = 0.0;
+    uint32_t fl = 0;
     if (live) {
-        const Tables *tb = s.tables;
-        const float *a_row = s_act + lane * A;
-        float *o_row = s_obs + lane * O;
-        const int k_soc = (p.pv ? 8 : 4);
-        const int k_dep = k_soc + n;
-
-        PairwiseSum pos, neg;
-        pos.init();
-        neg.init();
-        double pen_v = 0.0, nonexist = 0.0;
-        uint32_t fl = 0;
-        for (int c0 = 0; c0 < n; c0 += CH) {
-            if (c0 > 0) load_batch(c0);
+        for (int c0 = cbeg; c0 < cend; c0 += CH) {
+            if (c0 != cbeg) load_batch(c0);
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
-                if (c >= n) break;
-                const uint32_t wj = w[j];
-                double r = run[j];
-                const float a = a_row[c];
-
-                // penalise_charging_vehicles_outside_bounds (penaliser.py:39-57, 71-87): the vehicle's
-                // SoC and requested SoC at python index t-1; Python sum() order over the list.
-                if (t > 0 && (wj & W_PEN)) {
-                    const double req = p.req_stream ? s.req[(tbase + c) * (size_t)E + e] : 1.0;
-                    const double margin = 0.05 * req;
-                    if (r < req - margin) {
-                        const double d = (req - r) * 10;
-                        pen_v += d * d;
-                    }
-                }
-
-                // Charger.charge_or_discharge_vehicle (charger.py:37-56, 58-94, 108-144)
-                double pw = 0.0;
-                if (wj & W_OCC) {
-                    const double prev = (wj & W_STATIC) ? aux[j] : r;
-                    const double cap = (double)((wj >> W_CAP_SHIFT) & 0xffu);
-                    double nsoc = prev;
-                    if (a == 0.0f) {
-                        nsoc = prev;
-                    } else if (!p.bounded) {
-                        fl |= SNG_FLAG_CHARGING_MODE;
-                    } else {
-                        double pc, change;
-                        if (p.legacy) {               // NumPy < 2: float32 scalar * int -> float64
-                            pc = ((double)a * p.ev_power) * p.ev_eff;
-                            change = (pc * p.dt) / cap;
-                        } else {                      // NumPy 2 (NEP 50): float32 product
-                            const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
-                            const float pdt = __fmul_rn(pf, p.dt_f);
-                            pc = (double)pf;
-                            change = (double)pdt / cap;
-                        }
-                        const double calc = prev + change;
-                        if (a > 0.0f) {
-                            nsoc = (1.0 < calc) ? 1.0 : calc;                     // min(calc, 1.0)
-                            pw = pc;                                              // full power billed
-                        } else {
-                            pw = (calc >= 0.0) ? -((prev * cap) / p.dt) : pc;     // inverted flag, :122-132
-                            nsoc = (calc > 0.0) ? calc : 0.0;                     // max(0.0, calc)
-                        }
-                    }
-                    r = nsoc;
+                if (c >= cend) break;
+                const ChargerResult r = charger_step(p, w[j], aux[j], run[j], a_row[c], t,
+                                                     s.req + (tbase + c) * (size_t)E + e);
+                socv[(size_t)c * E + e] = r.soc;
+                o_row[k_soc + c] = (float)r.soc;
+                o_row[k_soc + n + c] = departure_obs(w[j]);
+                nonexist += r.nonexist;
+                fl |= r.fl;
+                if (L == 1) {
+                    pen_v += r.q;
+                    if (r.pw > 0.0) pos.push(r.pw);
+                    if (r.pw < 0.0) neg.push(r.pw);
                 } else {
-                    if (a != 0.0f) nonexist += 100.0;                             // reset_info_values, :146-156
-                    r = aux[j];                                                   // SOC[c, t] of an empty charger
+                    s_pw[le * n + c] = r.pw;
+                    s_q[le * n + c] = r.q;
                 }
-                socv[(size_t)c * E + e] = r;
+            }
+        }
+    }
+    if (L > 1) {
+        // gather the env's lanes: exact sums (multiples of 100) and flag bits, then in-order
+        // penalty / power sums by the leader from LDS
+#pragma unroll
+        for (int off = 1; off < L; off <<= 1) {
+            nonexist += __shfl_down(nonexist, off, L);
+            fl |= (uint32_t)__shfl_down((int)fl, off, L);
+        }
+        __syncthreads();
+        if (live && leader) {
+            for (int c = 0; c < n; ++c) {
+                const double pw = s_pw[le * n + c];
+                pen_v += s_q[le * n + c];
                 if (pw > 0.0) pos.push(pw);
                 if (pw < 0.0) neg.push(pw);
-
-                o_row[k_soc + c] = (float)r;
-                o_row[k_dep + c] = (float)((double)((wj >> W_DEP_SHIFT) & 0xffu) / 24);
             }
         }
+    }
+    if (live && leader) {
         if (t == 0) pen_v = s.pen0[e];
-
-        const double p_dis = neg.result();                                   // charging_station.py:293
-        const double p_ch = pos.result();                                    // :294
-        const double solar = p.pv ? tb->pv_power[t] * ratio : 0.0;           // central_management_system.py:99-103
-        const double demand = p_ch + p_dis;                                  // :105
-        if (demand < 0.0) fl |= p.v2x ? SNG_FLAG_V2X_BREAKPOINT : SNG_FLAG_NEGATIVE_DEMAND;
-        double rem = demand - solar;                                         // :167
-
-        // BatteryEnergyStorageSystem.charge_or_discharge (battery_energy_storage_system.py:186-262)
-        double pen_b = 0.0, bpow = 0.0, bcalc = 0.0;
-        if (p.bess) {
-            if (t == 0) s.bess0[e] = bess;                                   // :93-94
-            const double ba = (double)a_row[n];
-            if (ba == 0.0) {
-                bpow = 0.0;
-                bcalc = 0.0;
-            } else if (!p.bounded) {
-                fl |= SNG_FLAG_CHARGING_MODE;
-            } else if (ba > 0.0) {
-                const double avail = -rem;
-                const double cp = (ba * p.bess_pmax_ch) * p.bess_eff_ch;
-                const double calc = bess + (cp * p.dt) / p.bess_cap;
-                bcalc = cp;
-                bess = (1.0 < calc) ? 1.0 : calc;
-                bpow = cp;
-                rem = -(avail - cp);
-            } else {
-                double dp = (ba * p.bess_pmax_dis) * p.bess_eff_dis;
-                const double calc = bess + (dp * p.dt) / p.bess_cap;
-                bcalc = dp;
-                if (calc < 0.0) dp = -((bess * p.bess_cap) / p.dt);
-                bess = (calc > 0.0) ? calc : 0.0;
-                bpow = dp;
-                rem = rem + dp;
-            }
-            // penalise_battery_state_below_depth_of_discharge (penaliser.py:104-111)
-            if (bess < p.bess_dod) {
-                const double d = (p.bess_dod - bess) * 10;
-                pen_b = d * d;
-            } else if (!(bess <= 1.0)) {
-                fl |= SNG_FLAG_BESS_SOC_ABOVE_1;
-            }
-            s.bess[e] = bess;
-        }
-
-        // Accountant (accountant.py:213-227) and Penaliser totals (penaliser.py:177-187)
-        const double grid = rem;
-        const double energy = grid * p.dt;
-        const double price = tb->price[t];
-        const double cost = (energy < 0.0) ? (energy * p.sell_coef) * price : energy * price;
-        const double tot_pen = p.bat_pen_w * pen_b + pen_v;
-        const double total = p.grid_w * fabs(cost) + tot_pen;
-        reward[e] = -total;
-        done[e] = (t + 1 == p.T) ? 1 : 0;
-
-        write_obs_header(o_row, p, tb, t, ratio);
-        if (p.bess) o_row[k_dep + n] = (float)bess;
-
-        if (fl) s.flags[e] |= fl;
-        if (info.flags) info.flags[e] = fl;
-        if (info.episode_return) info.episode_return[e] += -total;
-        if (DIAG) {
-            if (info.grid_power) info.grid_power[e] = grid;
-            if (info.p_charge) info.p_charge[e] = p_ch;
-            if (info.p_discharge) info.p_discharge[e] = p_dis;
-            if (info.bess_soc) info.bess_soc[e] = p.bess ? bess : 0.0;
-            if (info.pen_vehicle) info.pen_vehicle[e] = pen_v;
-            if (info.pen_battery) info.pen_battery[e] = pen_b;
-            if (info.grid_cost) info.grid_cost[e] = cost;
-            if (info.total_cost) info.total_cost[e] = total;
-            if (info.solar) info.solar[e] = solar;
-            if (info.bess_power) info.bess_power[e] = bpow;
-            if (info.bess_calc_power) info.bess_calc_power[e] = bcalc;
-            if (info.nonexistent) info.nonexistent[e] = nonexist;
-            if (info.bess_initial) info.bess_initial[e] = p.bess ? s.bess0[e] : 0.0;
-        }
+        env_tail<DIAG>(p, s, info, e, t, ratio, bess, p.bess ? a_row[n] : 0.0f, pos.result(), neg.result(), pen_v,
+                       nonexist, fl, o_row, reward, done);
     }
     __syncthreads();
     copy_out(obs + e0 * O, s_obs, nblk * O, vec_io != 0, lane);
@@ -354,52 +430,52 @@ __global__ __launch_bounds__(kWave) void observe0_kernel(Params p, DeviceState s
     float *o_row = lds + lane * O;
     if (lane < nblk) {
         const double ratio = s.ratio[e];
-        int k = write_obs_header(o_row, p, s.tables, 0, ratio);
+        write_obs_header(o_row, p, s.tables, 0, ratio);
+        const int k = p.pv ? 8 : 4;
         for (int c = 0; c < n; ++c) {
             const size_t idx = (size_t)c * E + e;   // t = 0 slice
             const double aux = s.aux[idx];
             s.soc[idx] = aux;
             o_row[k + c] = (float)aux;
-            o_row[k + n + c] = (float)((double)((s.word[idx] >> W_DEP_SHIFT) & 0xffu) / 24);
+            o_row[k + n + c] = departure_obs(s.word[idx]);
         }
-        if (p.bess) o_row[k + 2 * n] = (float)s.bess[e];
+        if (p.bess) o_row[O - 1] = (float)s.bess[e];
         if (ep_return) ep_return[e] = 0.0;
     }
-    if (blockIdx.x == 0 && lane == 0) *s.episode += 1;   // next Philox day
+    if (blockIdx.x == 0 && lane == 0) *s.episode += 1;   // next device-RNG day
     __syncthreads();
     copy_out(obs + e0 * O, lds, nblk * O, vec_io != 0, lane);
 }
 
 // ---------------------------------------------------------------------------------
-// Device RNG day generator (same distributions as charging_station.py:200-279, Philox
-// draws).  Thread = (env, charger); writes the dense word/aux(/req) timeline.
+// Device RNG day generator: the reference's per-charger vehicle process
+// (charging_station.py:200-279: arrival with p = 0.4 when the charger is free, arrival SoC
+// U(0.1, 0.9), capacity U{15..119}, requested SoC, departure U{t+4/dt .. min(t+10/dt, T+1/dt)-1})
+// with counter-based SplitMix64 streams, one per (global env, charger, day).
+// Thread = (env, charger); writes the dense word / aux (/ req) timeline.
 // ---------------------------------------------------------------------------------
-struct Philox {
-    uint32_t k0, k1;
-    __device__ __forceinline__ uint4 operator()(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) const {
-        uint32_t key0 = k0, key1 = k1;
-#pragma unroll
-        for (int r = 0; r < 10; ++r) {
-            const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
-            const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
-            c0 = hi1 ^ c1 ^ key0;
-            c1 = lo1;
-            c2 = hi0 ^ c3 ^ key1;
-            c3 = lo0;
-            key0 += 0x9E3779B9u;
-            key1 += 0xBB67AE85u;
-        }
-        return make_uint4(c0, c1, c2, c3);
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+struct SplitMix {
+    uint64_t state;
+    __device__ __forceinline__ uint64_t next() {
+        state += 0x9e3779b97f4a7c15ull;
+        return splitmix64(state);
     }
 };
 
-__device__ __forceinline__ double u53(uint32_t a, uint32_t b) {
-    return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) / 9007199254740992.0;
-}
+__device__ __forceinline__ double u53(uint64_t x) { return (double)(x >> 11) * 0x1.0p-53; }
 
 __device__ __forceinline__ int below(uint32_t x, int n) {   // floor(x * n / 2^32)
     return (int)(((uint64_t)x * (uint64_t)n) >> 32);
 }
+
+// round(rand() - 0.1) == 1  <=>  rand() > 0.6: the 32-bit threshold ceil(0.6 * 2^32)
+constexpr uint32_t kArrivalThreshold = 2576980378u;
 
 __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
                                                          int i4, int i10, int i1) {
@@ -407,9 +483,8 @@ __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s
     const int c = blockIdx.y;
     if (e >= E) return;
     const uint64_t day = *s.episode;
-    const Philox rng{(uint32_t)seed, (uint32_t)(seed >> 32)};
-    const uint32_t ce = (uint32_t)(e + p.env_offset), cday = (uint32_t)day;   // global env id
-    uint32_t draw = 0;
+    const uint64_t ge = (uint64_t)(e + p.env_offset);   // global env id
+    SplitMix rng{splitmix64(splitmix64(splitmix64(seed ^ 0x5ee6c0deull) ^ ge) ^ ((uint64_t)c << 32 | (day & 0xffffffffull)))};
     const int T = p.T, n = p.n;
 
     bool present = false, prev_occ = false;
@@ -420,23 +495,23 @@ __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s
         bool arrived = false;
         double soc_arr = 0.0;
         if (!present) {
-            const uint4 x = rng(draw++, (uint32_t)c, ce, cday);
-            if ((u53(x.x, x.y) - 0.1) > 0.5) {                      // round(rand() - 0.1) == 1
+            const uint64_t x = rng.next();
+            if ((uint32_t)(x >> 32) >= kArrivalThreshold) {
                 arrived = true;
                 present = true;
-                soc_arr = 0.1 + (0.9 - 0.1) * u53(x.z, x.w);       // uniform(0.1, 0.9)
-                const uint4 y = rng(draw++, (uint32_t)c, ce, cday);
-                cap = p.diff_caps ? (uint32_t)(15 + below(y.x, 105)) : 40u;   // randint(15, 120)
-                if (p.req_enabled) {
-                    const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
-                    req = lo + (1.0 - lo) * u53(y.z, y.w);
-                } else {
-                    req = 1.0;
-                }
+                soc_arr = 0.1 + (0.9 - 0.1) * u53(rng.next());            // uniform(0.1, 0.9)
+                const uint64_t y = rng.next();
+                cap = p.diff_caps ? (uint32_t)(15 + below((uint32_t)(y >> 32), 105)) : 40u;   // randint(15, 120)
                 const int hi_c = t + i10, hi_d = T + i1;
                 const int high = hi_c < hi_d ? hi_c : hi_d;
                 const int low = t + i4;
-                dep = (low >= high) ? low : low + below(y.y, high - low);
+                dep = (low >= high) ? low : low + below((uint32_t)y, high - low);
+                if (p.req_enabled) {
+                    const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
+                    req = lo + (1.0 - lo) * u53(rng.next());
+                } else {
+                    req = 1.0;
+                }
             }
         }
         const bool occ = present && t < dep;
@@ -454,14 +529,14 @@ __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s
         const int rem = occ ? dep - t : 0;
         const size_t idx = ((size_t)t * n + c) * (size_t)E + e;
         s.word[idx] = pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem);
-        if (arrived || !occ) s.aux[idx] = arrived ? soc_arr : 0.0;
-        if (p.req_stream && pen) s.req[idx] = req;
+        s.aux[idx] = arrived ? soc_arr : 0.0;   // dense: full-line stores
+        if (p.req_stream) s.req[idx] = pen ? req : 0.0;
         prev_occ = occ;
         prev_rem = rem;
     }
     if (c == 0) {
-        const uint4 z = rng(0xFFFFFFFFu, 0xFFFFFFFFu, ce, cday);
-        s.ratio[e] = (double)below(z.x, 181) / 100;                 // random.randint(0, 180) / 100
+        SplitMix r2{splitmix64(splitmix64(seed ^ 0x7a71'0000ull) ^ ge ^ (day << 40))};
+        s.ratio[e] = (double)below((uint32_t)(r2.next() >> 32), 181) / 100;   // random.randint(0, 180) / 100
         s.pen0[e] = 0.0;
     }
 }
@@ -469,27 +544,36 @@ __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s
 // ---------------------------------------------------------------------------------
 // launch wrappers (called from sng_api.cpp)
 // ---------------------------------------------------------------------------------
-size_t step_lds_bytes(const Params &p) {
-    return (((size_t)kWave * p.act_dim + 3) & ~(size_t)3) * 4 + (size_t)kWave * p.obs_dim * 4;
-}
-
-// Optional start/stop events (ev != nullptr): hipExtLaunchKernel stamps them with the
-// dispatch's own begin/end timestamps, i.e. the kernel's device time.
+// Optional start/stop events: hipExtLaunchKernel stamps them with the dispatch's own
+// begin/end timestamps, i.e. the kernel's device time.
 struct LaunchEvents {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 
-template <int NC, bool DIAG>
+template <int NC, int L, bool DIAG>
 static void launch_step_t(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
                           double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
                           const LaunchEvents *ev) {
-    const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
+    constexpr int ENVS = kWave / L;
+    const dim3 grid((unsigned)((E + ENVS - 1) / ENVS)), block(kWave);
+    const uint32_t lds = (uint32_t)StepLds<L>::bytes(ENVS, p.act_dim, p.obs_dim, p.n);
     if (ev)
-        hipExtLaunchKernelGGL((step_kernel<NC, DIAG>), grid, block, (uint32_t)step_lds_bytes(p), stream, ev->start,
-                              ev->stop, 0u, p, s, info, act, obs, reward, done, E, t, vec_io);
+        hipExtLaunchKernelGGL((step_kernel<NC, L, DIAG>), grid, block, lds, stream, ev->start, ev->stop, 0u, p, s, info,
+                              act, obs, reward, done, E, t, vec_io);
     else
-        hipLaunchKernelGGL((step_kernel<NC, DIAG>), grid, block, step_lds_bytes(p), stream, p, s, info, act, obs,
-                           reward, done, E, t, vec_io);
+        hipLaunchKernelGGL((step_kernel<NC, L, DIAG>), grid, block, lds, stream, p, s, info, act, obs, reward, done, E,
+                           t, vec_io);
+}
+
+template <int NC, bool DIAG>
+static void launch_step_l(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
+                          double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
+                          const LaunchEvents *ev) {
+    switch (p.lanes) {
+        case 4: launch_step_t<NC, 4, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 2: launch_step_t<NC, 2, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        default: launch_step_t<NC, 1, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+    }
 }
 
 template <bool DIAG>
@@ -497,15 +581,20 @@ static void launch_step_n(const Params &p, const DeviceState &s, const InfoPtrs 
                           double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
                           const LaunchEvents *ev) {
     switch (p.n) {
-        case 1: launch_step_t<1, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
-        case 2: launch_step_t<2, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
-        case 4: launch_step_t<4, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
-        case 8: launch_step_t<8, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
-        case 10: launch_step_t<10, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
-        case 16: launch_step_t<16, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
-        case 50: launch_step_t<50, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
-        default: launch_step_t<0, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 1: launch_step_t<1, 1, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 2: launch_step_l<2, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 4: launch_step_l<4, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 8: launch_step_l<8, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 10: launch_step_l<10, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 16: launch_step_l<16, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 50: launch_step_l<50, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        default: launch_step_t<0, 1, DIAG>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev); break;
     }
+}
+
+int step_lanes_supported(int n, int lanes) {
+    const bool multi = (n == 2 || n == 4 || n == 8 || n == 10 || n == 16 || n == 50);
+    return (lanes == 1 || (multi && (lanes == 2 || lanes == 4))) ? 1 : 0;
 }
 
 hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
@@ -526,7 +615,7 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
                            int vec_io, hipStream_t stream) {
     const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
-    const size_t lds = (size_t)kWave * p.obs_dim * 4;
+    const size_t lds = (size_t)round4(kWave * p.obs_dim) * 4;
     hipLaunchKernelGGL(observe0_kernel, grid, block, lds, stream, p, s, obs, ep_return, E, vec_io);
     return hipGetLastError();
 }

@@ -73,6 +73,7 @@ struct Params {
     double bess_cap, bess_pmax_ch, bess_pmax_dis, bess_eff_ch, bess_eff_dis, bess_dod;
     double grid_w, bat_pen_w, sell_coef;
     int64_t env_offset;       // global index of env 0 of this handle (sharded runs)
+    int32_t lanes;            // step kernel: lanes per environment (1, 2 or 4)
 };
 
 struct DeviceState {

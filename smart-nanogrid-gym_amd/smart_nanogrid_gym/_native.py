@@ -61,6 +61,7 @@ class SngConfig(ctypes.Structure):
         ("ev_efficiency", ctypes.c_double),
         ("irradiance_per_minute", c_double_p),
         ("irradiance_minutes", ctypes.c_int64),
+        ("step_lanes_per_env", ctypes.c_int32),
     ]
 
 

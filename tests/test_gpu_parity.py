@@ -105,16 +105,17 @@ def _oracle_batch(kw, seed, idx):
     return cfg, [O.OracleEnv(cfg, seed + int(i)) for i in idx]
 
 
-@pytest.mark.parametrize("E,N,mode", [(4096, 10, "sparse"), (4096, 10, "dense"), (1024, 50, "sparse"),
-                                      (1000, 4, "on_departure"), (333, 1, "sparse")])
-def test_batched_reference_rng_vs_oracle_bit_exact(E, N, mode):
+@pytest.mark.parametrize("E,N,mode,lanes", [(4096, 10, "sparse", 1), (4096, 10, "sparse", 2), (4096, 10, "dense", 4),
+                                            (1024, 50, "sparse", 0), (1024, 50, "dense", 4), (1000, 4, "on_departure", 2),
+                                            (333, 1, "sparse", 0), (777, 7, "dense", 0), (300, 16, "sparse", 4)])
+def test_batched_reference_rng_vs_oracle_bit_exact(E, N, mode, lanes):
     """Config 2 (4,096 envs x 10 chargers x 24 steps): every env against the oracle seeded base+i,
     two consecutive days, random actions with 20 % exact zeros."""
     kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
               vehicle_uncharged_penalty_mode=mode)
     seed = 1000 + N
     O.lib().orc_set_square_mode(1)
-    venv = SmartNanogridVecEnv(E, seed=seed, rng="reference", **kw)
+    venv = SmartNanogridVecEnv(E, seed=seed, rng="reference", step_lanes_per_env=lanes, **kw)
     cfg, envs = _oracle_batch(kw, seed, range(E))
     rng = np.random.default_rng(E + N)
     for day in range(2):
