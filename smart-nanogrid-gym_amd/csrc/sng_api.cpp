@@ -249,8 +249,8 @@ bool encode_day(const Params &p, int64_t E, int64_t e, const DayView &d, uint32_
             double a = 0.0;
             if (occupied) {
                 const double cv = cap[prev];
-                if (!(cv >= 0.0 && cv <= 255.0 && cv == std::floor(cv))) {
-                    err = "vehicle capacities must be integers in [0, 255]";
+                if (!(cv >= 1.0 && cv <= 255.0 && cv == std::floor(cv))) {
+                    err = "vehicle capacities of occupied chargers must be integers in [1, 255]";
                     return false;
                 }
                 capv = (uint32_t)cv;
@@ -535,6 +535,11 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
     p.act_dim = p.n + p.bess;                          // :110-127
     p.dt = c.time_interval_hours;
     p.dt_f = (float)c.time_interval_hours;
+    {
+        int ex = 0;
+        p.dt_pow2 = (std::frexp(p.dt, &ex) == 0.5) ? 1 : 0;   // dt = 2^k: x / dt == x * 2^-k
+        p.rdt = 1.0 / p.dt;
+    }
     p.ev_power = c.ev_max_power_kw;
     p.ev_eff = c.ev_efficiency;
     p.ev_power_f = (float)c.ev_max_power_kw;
@@ -555,7 +560,7 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
         }
         p.lanes = c.step_lanes_per_env;
     } else {
-        p.lanes = step_lanes_supported(p.n, 2) ? 2 : 1;   // tuned on MI355X at N=10, E=65,536
+        p.lanes = 1;   // tuned on MI355X at N=10, E=65,536 (tools/gpu_session.sh sweep)
     }
     env->i4 = (int)(4 / p.dt);
     env->i10 = (int)(10 / p.dt);
@@ -574,6 +579,8 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
         ht.price[k] = env->tables.price[k];
         ht.price_norm[k] = env->tables.price[k] / env->tables.price_max;   // accountant.py:229-233
     }
+    ht.recip[0] = 0.0;
+    for (int c = 1; c < 256; ++c) ht.recip[c] = 1.0 / (double)c;
 
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) {

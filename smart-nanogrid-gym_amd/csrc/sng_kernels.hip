@@ -1,20 +1,21 @@
 // sng_kernels.hip -- HIP kernels of the batched SmartNanogridEnv hot path (gfx950).
 //
-// Step kernel mapping: L lanes per environment (L = 1, 2 or 4), 64/L environments per
-// 64-thread workgroup (one wavefront).  Lane `part` of an env owns a contiguous range of
-// chargers; the env's first lane (the leader) finishes the env (sums, BESS, cost, reward).
-// With L > 1 a 65,536-env step runs 2048-4096 wavefronts instead of 1024, which is what
-// keeps enough HBM requests in flight on 256 CUs.
+// Step kernel mapping: 256-thread workgroups (4 wavefronts); L lanes per environment
+// (L = 1, 2 or 4), 256/L environments per workgroup.  Lane `part` of an env owns a
+// contiguous range of chargers; the env's first lane (the leader) finishes the env (sums,
+// BESS, cost, reward).  256-thread workgroups dispatch 4x fewer workgroups than one-wave
+// groups (measured: the 1024 one-wave groups of a 65,536-env step took ~2 us just to start).
 //
 // Per-env state is SoA with the env index fastest (sng_layout.h), so every per-charger
 // load/store of a wavefront is a contiguous run.  The policy-facing row-major actions
 // [E][A] and observations [E][O] are staged through LDS so their HBM side is a contiguous,
 // 16-byte-per-lane stream.
 //
-// Arithmetic follows the reference operation for operation (built with -ffp-contract=off).
-// Sums over chargers use the reference's order: numpy's pairwise sum for the charging
-// powers (charging_station.py:293-294) and Python's left-to-right sum() for the vehicle
-// penalties (penaliser.py:55).
+// Arithmetic follows the reference operation for operation (built with -ffp-contract=off;
+// the two explicit fma-based divisions below are exact, see their comments).  Sums over
+// chargers use the reference's order: numpy's pairwise sum for the charging powers
+// (charging_station.py:293-294) and Python's left-to-right sum() for the vehicle penalties
+// (penaliser.py:55).
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -26,10 +27,25 @@ namespace sng {
 
 constexpr int kWave = 64;
 
+#ifdef SNG_STAMPS
+// Diagnostic build only (make stamps): per-workgroup s_memrealtime stamps (100 MHz) at the
+// phase boundaries of the step kernel -> g_stamps[block*4 + k].  Never compiled into libsng.so.
+__device__ unsigned long long *g_stamps;
+#define SNG_STAMP(k)                                                                                 \
+    do {                                                                                             \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                  \
+        const unsigned long long ts_ = __builtin_amdgcn_s_memrealtime();                             \
+        if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 4 + (k)] = ts_;              \
+    } while (0)
+#else
+#define SNG_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 // ---------------------------------------------------------------------------------
 // numpy pairwise_sum (loops_utils.h.src) for n <= 128, fed one element at a time in
-// array order.  Elements are buffered per block of 8; a block that completes is folded
-// into the 8 running accumulators, the last partial block is the sequential tail.
+// array order (used for N > 16; smaller N use the LDS-compacted form below).
 // ---------------------------------------------------------------------------------
 struct PairwiseSum {
     double r[8];
@@ -64,56 +80,75 @@ struct PairwiseSum {
     }
 };
 
+// The same sum over a compacted array the lane has written to its own LDS row:
+// n < 8 is the sequential sum `seq` the caller kept on the fly (adding the skipped +0.0
+// terms is exact); otherwise 8 accumulators over full blocks, pairwise tree, sequential tail.
+__device__ __forceinline__ double pairwise_row(const double *row, int n, double seq) {
+    if (n < 8) return seq;
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] = row[j];
+    const int full = n - (n & 7);
+    for (int i = 8; i < full; i += 8) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) r[j] += row[i + j];
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int i = full; i < n; ++i) res += row[i];
+    return res;
+}
+
 __host__ __device__ constexpr int round4(int x) { return (x + 3) & ~3; }
 
-// Copy `count` floats global -> LDS with 16 B per lane when the run is aligned.  Each lane
+// Copy `count` floats global -> LDS with 16 B per lane when the run is aligned.  Each thread
 // issues up to K loads before the first LDS write (clamped, unconditional loads: no per-element
-// branch + wait), so the whole copy is one HBM round trip when count <= K * 256 floats.
-template <int K>
+// branch + wait), so the whole copy is one HBM round trip when count <= K * 4 * BLOCK floats.
+template <int K, int BLOCK>
 __device__ __forceinline__ void copy_in(float *__restrict__ dst, const float *__restrict__ src, int count,
-                                        bool vec, int lane) {
+                                        bool vec, int tid) {
     if (vec && (count & 3) == 0) {
         const float4 *s4 = reinterpret_cast<const float4 *>(src);
         float4 *d4 = reinterpret_cast<float4 *>(dst);
         const int n4 = count >> 2;
-        for (int base = 0; base < n4; base += K * kWave) {
+        for (int base = 0; base < n4; base += K * BLOCK) {
             float4 v[K];
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-                const int i = base + k * kWave + lane;
+                const int i = base + k * BLOCK + tid;
                 v[k] = s4[i < n4 ? i : n4 - 1];
             }
 #pragma unroll
-            for (int k = 0; k < K; ++k) {   // out-of-range lanes rewrite the last element (same value)
-                const int i = base + k * kWave + lane;
+            for (int k = 0; k < K; ++k) {   // out-of-range threads rewrite the last element (same value)
+                const int i = base + k * BLOCK + tid;
                 d4[i < n4 ? i : n4 - 1] = v[k];
             }
         }
     } else {
-        for (int base = 0; base < count; base += 4 * K * kWave) {
+        for (int base = 0; base < count; base += 4 * K * BLOCK) {
             float v[4 * K];
 #pragma unroll
             for (int k = 0; k < 4 * K; ++k) {
-                const int i = base + k * kWave + lane;
+                const int i = base + k * BLOCK + tid;
                 v[k] = src[i < count ? i : count - 1];
             }
 #pragma unroll
             for (int k = 0; k < 4 * K; ++k) {
-                const int i = base + k * kWave + lane;
+                const int i = base + k * BLOCK + tid;
                 dst[i < count ? i : count - 1] = v[k];
             }
         }
     }
 }
 
+template <int BLOCK>
 __device__ __forceinline__ void copy_out(float *__restrict__ dst, const float *__restrict__ src, int count,
-                                         bool vec, int lane) {
+                                         bool vec, int tid) {
     if (vec && (count & 3) == 0) {
         const float4 *s4 = reinterpret_cast<const float4 *>(src);
         float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int i = lane; i < (count >> 2); i += kWave) d4[i] = s4[i];
+        for (int i = tid; i < (count >> 2); i += BLOCK) d4[i] = s4[i];
     } else {
-        for (int i = lane; i < count; i += kWave) dst[i] = src[i];
+        for (int i = tid; i < count; i += BLOCK) dst[i] = src[i];
     }
 }
 
@@ -132,10 +167,24 @@ __device__ __forceinline__ void write_obs_header(float *o, const Params &p, cons
 }
 
 // Remaining time to departure / 24 (smart_nanogrid_environment.py:216-217) as float32.
-// (float)((double)d / 24) equals the correctly rounded float32 quotient for every integer d < 256
-// (d/24 is never a float32 rounding midpoint), so the cheaper float32 division is exact here.
+// The reference rounds d / 24 in float64 and then to float32; for integers d < 256 that equals the
+// correctly rounded float32 quotient (d/24 is never a float32 rounding midpoint), which
+// q = d*r; q + fma(-q, 24, d)*r reproduces for every d < 256 (checked exhaustively).
 __device__ __forceinline__ float departure_obs(uint32_t w) {
-    return (float)((w >> W_DEP_SHIFT) & 0xffu) / 24.0f;
+    const float d = (float)((w >> W_DEP_SHIFT) & 0xffu);
+    constexpr float r24 = 1.0f / 24.0f;
+    const float q = d * r24;
+    return __builtin_fmaf(__builtin_fmaf(-q, 24.0f, d), r24, q);
+}
+
+// x / c for a float32-valued x and an integer c in [1, 255] with r = fl(1/c):
+// q = x*r, remainder fma(-q, c, x) (exact), q' = fma(rem, r, q).  x/c is never a float64
+// rounding midpoint and lies >= ulp/(2c) from one, while q' differs from x/c by < 2^-50 ulp,
+// so q' is the correctly rounded quotient -- bitwise equal to x / c.  Checked exhaustively for
+// every float32 mantissa and every c (tools/check_division.c; scaling by 2^k is exact).
+__device__ __forceinline__ double div_by_cap(double x, double c, double r) {
+    const double q = x * r;
+    return __builtin_fma(__builtin_fma(-q, c, x), r, q);
 }
 
 // ---------------------------------------------------------------------------------
@@ -152,50 +201,49 @@ struct ChargerResult {
     uint32_t fl;
 };
 
-__device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, float a,
-                                                      int t, const double *__restrict__ req_ptr) {
-    ChargerResult o{0.0, 0.0, run, 0.0, 0u};
-    if (t > 0 && (w & W_PEN)) {
-        const double req = p.req_stream ? *req_ptr : 1.0;
-        const double margin = 0.05 * req;
-        if (run < req - margin) {
-            const double d = (req - run) * 10;
-            o.q = d * d;
-        }
+// Written with selects rather than branches so the chargers of an env interleave (ILP hides the
+// f64 latency at one wavefront per SIMD); only the inverted-flag discharge keeps a (divergent)
+// branch for its division when dt is not a power of two.  Occupied chargers have cap in [1, 255]
+// (validated when a scenario is encoded).
+__device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, double req,
+                                                      float a, int t, const double *__restrict__ s_rcp) {
+    ChargerResult o;
+    const double margin = 0.05 * req;
+    const double d = (req - run) * 10;
+    const bool insufficient = (t > 0) && (w & W_PEN) && (run < req - margin);
+    o.q = insufficient ? d * d : 0.0;
+
+    const bool occ = (w & W_OCC) != 0;
+    const double prev = (w & W_STATIC) ? aux : run;
+    const uint32_t capi = (w >> W_CAP_SHIFT) & 0xffu;
+    const double cap = (double)capi;
+    const bool idle = (a == 0.0f);
+    const bool chg = (a > 0.0f);
+    double pc, change;
+    if (p.legacy) {   // NumPy < 2: float32 scalar * int -> float64 (float64 numerator: plain division)
+        pc = ((double)a * p.ev_power) * p.ev_eff;
+        change = (pc * p.dt) / cap;
+    } else {          // NumPy 2 (NEP 50): float32 product
+        const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
+        const float pdt = __fmul_rn(pf, p.dt_f);
+        pc = (double)pf;
+        change = div_by_cap((double)pdt, cap, s_rcp[capi]);
     }
-    if (w & W_OCC) {
-        const double prev = (w & W_STATIC) ? aux : run;
-        const double cap = (double)((w >> W_CAP_SHIFT) & 0xffu);
-        double nsoc = prev;
-        if (a == 0.0f) {
-            nsoc = prev;
-        } else if (!p.bounded) {
-            o.fl |= SNG_FLAG_CHARGING_MODE;
-        } else {
-            double pc, change;
-            if (p.legacy) {   // NumPy < 2: float32 scalar * int -> float64
-                pc = ((double)a * p.ev_power) * p.ev_eff;
-                change = (pc * p.dt) / cap;
-            } else {          // NumPy 2 (NEP 50): float32 product
-                const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
-                const float pdt = __fmul_rn(pf, p.dt_f);
-                pc = (double)pf;
-                change = (double)pdt / cap;
-            }
-            const double calc = prev + change;
-            if (a > 0.0f) {
-                nsoc = (1.0 < calc) ? 1.0 : calc;                     // min(calc, 1.0)
-                o.pw = pc;                                            // full power billed
-            } else {
-                o.pw = (calc >= 0.0) ? -((prev * cap) / p.dt) : pc;   // inverted flag, :122-132
-                nsoc = (calc > 0.0) ? calc : 0.0;                     // max(0.0, calc)
-            }
-        }
-        o.soc = nsoc;
-    } else {
-        if (a != 0.0f) o.nonexist = 100.0;
-        o.soc = aux;   // SOC[c, t] of an empty charger
+    const double calc = prev + change;
+    double pw_dis = pc;                                          // inverted flag, charger.py:122-132
+    if (occ && !idle && !chg && calc >= 0.0) {
+        const double x = prev * cap;
+        pw_dis = -(p.dt_pow2 ? x * p.rdt : x / p.dt);
     }
+    const double soc_chg = (1.0 < calc) ? 1.0 : calc;           // min(calc, 1.0)
+    const double soc_dis = (calc > 0.0) ? calc : 0.0;           // max(0.0, calc)
+    const bool act = !idle && p.bounded;
+    const double nsoc = act ? (chg ? soc_chg : soc_dis) : prev;
+    const double pw = act ? (chg ? pc : pw_dis) : 0.0;          // full power billed when charging
+    o.soc = occ ? nsoc : aux;                                   // empty charger: SOC[c, t] as recorded
+    o.pw = occ ? pw : 0.0;
+    o.nonexist = (!occ && !idle) ? 100.0 : 0.0;
+    o.fl = (occ && !idle && !p.bounded) ? (uint32_t)SNG_FLAG_CHARGING_MODE : 0u;
     return o;
 }
 
@@ -282,18 +330,31 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     }
 }
 
-// LDS layout of the step kernel for ENVS envs per workgroup.
-template <int L>
+// Workgroup size of the step kernel: 256 threads (4 wavefronts, 4x fewer workgroups to
+// dispatch) while the LDS staging fits, one wavefront for wide stations (N > 16 or runtime N)
+// so the [ENVS][O] observation tile stays well inside the 160 KB LDS.
+__host__ __device__ constexpr int step_block(int NC) { return (NC > 0 && NC <= 16) ? 256 : 64; }
+
+// LDS carve-up of the step kernel (every region 16-byte aligned):
+//   act [ENVS][A] f32 | obs [ENVS][O] f32 | rcp [256] f64 | pos [ENVS][NC] f64 | neg [ENVS][NC] f64
+//   | (L > 1) pw [ENVS][NC] f64 | q [ENVS][NC] f64
+template <int NC, int L>
 struct StepLds {
-    __host__ __device__ static int act_floats(int envs, int A) { return round4(envs * A); }
-    __host__ __device__ static int obs_floats(int envs, int O) { return round4(envs * O); }
-    __host__ __device__ static size_t bytes(int envs, int A, int O, int n) {
-        return (size_t)(act_floats(envs, A) + obs_floats(envs, O)) * 4 + (L > 1 ? (size_t)2 * envs * n * 8 : 0);
+    static constexpr int BLOCK = step_block(NC);
+    static constexpr int ENVS = BLOCK / L;
+    static constexpr bool kRows = NC > 0 && NC <= 16;   // compacted power rows (else PairwiseSum)
+    __host__ __device__ static int act_floats(int A) { return round4(ENVS * A); }
+    __host__ __device__ static int obs_floats(int O) { return round4(ENVS * O); }
+    __host__ __device__ static size_t bytes(int A, int O) {
+        size_t b = (size_t)(act_floats(A) + obs_floats(O)) * 4 + 256 * 8;
+        if (kRows) b += (size_t)2 * ENVS * NC * 8;
+        if (L > 1) b += (size_t)2 * ENVS * NC * 8;
+        return b;
     }
 };
 
 // ---------------------------------------------------------------------------------
-// The fused step: SmartNanogridEnv.step(actions) for 64/L envs per workgroup.
+// The fused step: SmartNanogridEnv.step(actions) for BLOCK/L envs per workgroup.
 // NC   = compile-time charger count (0: runtime p.n, L must be 1);
 // L    = lanes per env;
 // DIAG = also write the per-step diagnostics (SngInfo arrays).
@@ -301,36 +362,43 @@ struct StepLds {
 // batch before the action staging wait, so one lane keeps 3*CH + 2 requests in flight.
 // ---------------------------------------------------------------------------------
 template <int NC, int L, bool DIAG>
-__global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, InfoPtrs info,
-                                                     const float *__restrict__ act, float *__restrict__ obs,
-                                                     double *__restrict__ reward, uint8_t *__restrict__ done,
-                                                     int64_t E, int t, int vec_io) {
+__global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceState s, InfoPtrs info,
+                                                              const float *__restrict__ act, float *__restrict__ obs,
+                                                              double *__restrict__ reward, uint8_t *__restrict__ done,
+                                                              int64_t E, int t, int vec_io) {
     static_assert(L == 1 || NC > 0, "multi-lane envs need a compile-time charger count");
-    constexpr int ENVS = kWave / L;
+    using Lay = StepLds<NC, L>;
+    constexpr int BLOCK = Lay::BLOCK;
+    constexpr int ENVS = Lay::ENVS;
+    constexpr bool kRows = Lay::kRows;
     constexpr int CH = (L > 1) ? (NC + L - 1) / L : ((NC > 0 && NC <= 16) ? NC : 8);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int n = NC ? NC : p.n;
     const int A = p.act_dim, O = p.obs_dim;
-    const int lane = threadIdx.x;
-    const int le = lane / L, part = lane % L;
+    const int tid = threadIdx.x;
+    const int le = tid / L, part = tid % L;
     const int64_t e0 = (int64_t)blockIdx.x * ENVS;
     const int nblk = (int)((E - e0) < ENVS ? (E - e0) : ENVS);
     const int64_t e = e0 + le;
     const bool live = le < nblk;
     const bool leader = part == 0;
     float *s_act = lds;
-    float *s_obs = lds + StepLds<L>::act_floats(ENVS, A);
-    double *s_pw = reinterpret_cast<double *>(s_obs + StepLds<L>::obs_floats(ENVS, O));   // [ENVS][n], L > 1
-    double *s_q = s_pw + ENVS * n;
+    float *s_obs = lds + Lay::act_floats(A);
+    double *s_rcp = reinterpret_cast<double *>(s_obs + Lay::obs_floats(O));
+    double *s_pos = s_rcp + 256;                                  // [ENVS][NC] compacted positive powers
+    double *s_neg = s_pos + (kRows ? ENVS * NC : 0);              // [ENVS][NC] compacted negative powers
+    double *s_pw = s_neg + (kRows ? ENVS * NC : 0);               // [ENVS][NC] per-charger powers (L > 1)
+    double *s_q = s_pw + (L > 1 ? ENVS * NC : 0);                 // [ENVS][NC] per-charger penalty terms
     const uint32_t *__restrict__ word = s.word;
     const double *__restrict__ auxv = s.aux;
+    const double *__restrict__ reqv = s.req;
     double *__restrict__ socv = s.soc;
     const size_t tbase = (size_t)t * n;
     const int cbeg = (L > 1) ? part * CH : 0;
     const int cend = (L > 1) ? ((cbeg + CH) < n ? (cbeg + CH) : n) : n;
 
     uint32_t w[CH];
-    double aux[CH], run[CH];
+    double aux[CH], run[CH], req[CH];
     auto load_batch = [&](int c0) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
@@ -340,6 +408,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
                 w[j] = word[idx];
                 aux[j] = auxv[idx];
                 run[j] = socv[(size_t)c * E + e];
+                req[j] = p.req_stream ? reqv[idx] : 1.0;
             }
         }
     };
@@ -352,15 +421,43 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
         }
         load_batch(cbeg);
     }
-    copy_in<(NC > 0 && NC < 16) ? 4 : 8>(s_act, act + e0 * A, nblk * A, vec_io != 0, lane);
+#ifdef SNG_STAMPS
+    if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
+#endif
+#pragma unroll
+    for (int i = tid; i < 256; i += BLOCK) s_rcp[i] = s.tables->recip[i];
+    copy_in<(NC > 0 && NC < 16) ? 4 : 8, BLOCK>(s_act, act + e0 * A, nblk * A, vec_io != 0, tid);
     __syncthreads();
+    SNG_STAMP(1);
 
     const float *a_row = s_act + le * A;
     float *o_row = s_obs + le * O;
     const int k_soc = (p.pv ? 8 : 4);
     PairwiseSum pos, neg;
-    pos.init();
-    neg.init();
+    double seq_pos = 0.0, seq_neg = 0.0;
+    int n_pos = 0, n_neg = 0;
+    double *row_pos = s_pos + le * NC, *row_neg = s_neg + le * NC;
+    if (!kRows) {
+        pos.init();
+        neg.init();
+    }
+    // one power into the pairwise-sum state (numpy order: compacted array of positives/negatives).
+    // Rows: unconditional LDS stores at the current count (a slot is overwritten until its element
+    // is kept) and select-based counters, so nothing here is addressed through a pointer select.
+    auto add_power = [&](double pw) {
+        if (kRows) {
+            const bool ip = pw > 0.0, in = pw < 0.0;
+            row_pos[n_pos] = pw;
+            row_neg[n_neg] = pw;
+            seq_pos = ip ? seq_pos + pw : seq_pos;
+            seq_neg = in ? seq_neg + pw : seq_neg;
+            n_pos += ip ? 1 : 0;
+            n_neg += in ? 1 : 0;
+        } else {
+            if (pw > 0.0) pos.push(pw);
+            if (pw < 0.0) neg.push(pw);
+        }
+    };
     double pen_v = 0.0, nonexist = 0.0;
     uint32_t fl = 0;
     if (live) {
@@ -370,8 +467,7 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
                 if (c >= cend) break;
-                const ChargerResult r = charger_step(p, w[j], aux[j], run[j], a_row[c], t,
-                                                     s.req + (tbase + c) * (size_t)E + e);
+                const ChargerResult r = charger_step(p, w[j], aux[j], run[j], req[j], a_row[c], t, s_rcp);
                 socv[(size_t)c * E + e] = r.soc;
                 o_row[k_soc + c] = (float)r.soc;
                 o_row[k_soc + n + c] = departure_obs(w[j]);
@@ -379,11 +475,10 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
                 fl |= r.fl;
                 if (L == 1) {
                     pen_v += r.q;
-                    if (r.pw > 0.0) pos.push(r.pw);
-                    if (r.pw < 0.0) neg.push(r.pw);
+                    add_power(r.pw);
                 } else {
-                    s_pw[le * n + c] = r.pw;
-                    s_q[le * n + c] = r.q;
+                    s_pw[le * NC + c] = r.pw;
+                    s_q[le * NC + c] = r.q;
                 }
             }
         }
@@ -398,37 +493,47 @@ __global__ __launch_bounds__(kWave) void step_kernel(Params p, DeviceState s, In
         }
         __syncthreads();
         if (live && leader) {
-            for (int c = 0; c < n; ++c) {
-                const double pw = s_pw[le * n + c];
-                pen_v += s_q[le * n + c];
-                if (pw > 0.0) pos.push(pw);
-                if (pw < 0.0) neg.push(pw);
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                pen_v += s_q[le * NC + c];
+                add_power(s_pw[le * NC + c]);
             }
         }
     }
     if (live && leader) {
         if (t == 0) pen_v = s.pen0[e];
-        env_tail<DIAG>(p, s, info, e, t, ratio, bess, p.bess ? a_row[n] : 0.0f, pos.result(), neg.result(), pen_v,
-                       nonexist, fl, o_row, reward, done);
+        double p_ch, p_dis;
+        if (kRows) {
+            p_ch = pairwise_row(row_pos, n_pos, seq_pos);
+            p_dis = pairwise_row(row_neg, n_neg, seq_neg);
+        } else {
+            p_ch = pos.result();
+            p_dis = neg.result();
+        }
+        env_tail<DIAG>(p, s, info, e, t, ratio, bess, p.bess ? a_row[n] : 0.0f, p_ch, p_dis, pen_v, nonexist, fl,
+                       o_row, reward, done);
     }
     __syncthreads();
-    copy_out(obs + e0 * O, s_obs, nblk * O, vec_io != 0, lane);
+    SNG_STAMP(2);
+    copy_out<BLOCK>(obs + e0 * O, s_obs, nblk * O, vec_io != 0, tid);
+    SNG_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------------
 // Observation at t = 0 after a reset (SmartNanogridEnv.reset -> __get_observations,
 // smart_nanogrid_environment.py:358-360): SOC[c, 0] as generated, departure times at 0.
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(kWave) void observe0_kernel(Params p, DeviceState s, float *__restrict__ obs,
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s, float *__restrict__ obs,
                                                          double *__restrict__ ep_return, int64_t E, int vec_io) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int n = p.n, O = p.obs_dim;
-    const int lane = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * kWave;
-    const int nblk = (int)((E - e0) < kWave ? (E - e0) : kWave);
-    const int64_t e = e0 + lane;
-    float *o_row = lds + lane * O;
-    if (lane < nblk) {
+    const int tid = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * BLOCK;
+    const int nblk = (int)((E - e0) < BLOCK ? (E - e0) : BLOCK);
+    const int64_t e = e0 + tid;
+    float *o_row = lds + tid * O;
+    if (tid < nblk) {
         const double ratio = s.ratio[e];
         write_obs_header(o_row, p, s.tables, 0, ratio);
         const int k = p.pv ? 8 : 4;
@@ -442,9 +547,9 @@ __global__ __launch_bounds__(kWave) void observe0_kernel(Params p, DeviceState s
         if (p.bess) o_row[O - 1] = (float)s.bess[e];
         if (ep_return) ep_return[e] = 0.0;
     }
-    if (blockIdx.x == 0 && lane == 0) *s.episode += 1;   // next device-RNG day
+    if (blockIdx.x == 0 && tid == 0) *s.episode += 1;   // next device-RNG day
     __syncthreads();
-    copy_out(obs + e0 * O, lds, nblk * O, vec_io != 0, lane);
+    copy_out<BLOCK>(obs + e0 * O, lds, nblk * O, vec_io != 0, tid);
 }
 
 // ---------------------------------------------------------------------------------
@@ -554,9 +659,9 @@ template <int NC, int L, bool DIAG>
 static void launch_step_t(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
                           double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
                           const LaunchEvents *ev) {
-    constexpr int ENVS = kWave / L;
-    const dim3 grid((unsigned)((E + ENVS - 1) / ENVS)), block(kWave);
-    const uint32_t lds = (uint32_t)StepLds<L>::bytes(ENVS, p.act_dim, p.obs_dim, p.n);
+    using Lay = StepLds<NC, L>;
+    const dim3 grid((unsigned)((E + Lay::ENVS - 1) / Lay::ENVS)), block(Lay::BLOCK);
+    const uint32_t lds = (uint32_t)Lay::bytes(p.act_dim, p.obs_dim);
     if (ev)
         hipExtLaunchKernelGGL((step_kernel<NC, L, DIAG>), grid, block, lds, stream, ev->start, ev->stop, 0u, p, s, info,
                               act, obs, reward, done, E, t, vec_io);
@@ -592,6 +697,12 @@ static void launch_step_n(const Params &p, const DeviceState &s, const InfoPtrs 
     }
 }
 
+#ifdef SNG_STAMPS
+extern "C" int sng_debug_set_stamps(unsigned long long *dev_ptr) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int step_lanes_supported(int n, int lanes) {
     const bool multi = (n == 2 || n == 4 || n == 8 || n == 10 || n == 16 || n == 50);
     return (lanes == 1 || (multi && (lanes == 2 || lanes == 4))) ? 1 : 0;
@@ -614,9 +725,15 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
 
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
                            int vec_io, hipStream_t stream) {
-    const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
-    const size_t lds = (size_t)round4(kWave * p.obs_dim) * 4;
-    hipLaunchKernelGGL(observe0_kernel, grid, block, lds, stream, p, s, obs, ep_return, E, vec_io);
+    if ((size_t)round4(256 * p.obs_dim) * 4 <= 64 * 1024) {
+        const dim3 grid((unsigned)((E + 255) / 256)), block(256);
+        hipLaunchKernelGGL(observe0_kernel<256>, grid, block, (size_t)round4(256 * p.obs_dim) * 4, stream, p, s, obs,
+                           ep_return, E, vec_io);
+    } else {
+        const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
+        hipLaunchKernelGGL(observe0_kernel<kWave>, grid, block, (size_t)round4(kWave * p.obs_dim) * 4, stream, p, s,
+                           obs, ep_return, E, vec_io);
+    }
     return hipGetLastError();
 }
 

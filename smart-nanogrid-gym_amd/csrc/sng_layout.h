@@ -56,6 +56,7 @@ struct Tables {
     double pv_power[4 * kMaxT];    // available_solar_power[k]  (:375-379)
     double price[kPriceLen];       // energy_price[0, k]        (accountant.py:225-227)
     double price_norm[kPriceLen];  // energy_price / max        (:229-233)
+    double recip[256];             // 1.0 / c (correctly rounded), c = vehicle capacity; recip[0] = 0
     int32_t n_irr;
 };
 
@@ -67,6 +68,8 @@ struct Params {
     int32_t pv, bess, v2x, bounded, legacy, req_stream, penalty_mode;
     int32_t diff_caps, req_enabled;
     double dt;
+    double rdt;               // 1 / dt, used only when dt is a power of two (x * rdt == x / dt exactly)
+    int32_t dt_pow2;
     float dt_f;               // float32(dt) for the NEP 50 float32 product
     float ev_power_f, ev_eff_f;
     double ev_power, ev_eff;
