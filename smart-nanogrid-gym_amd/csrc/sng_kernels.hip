@@ -154,16 +154,26 @@ __device__ __forceinline__ void copy_out(float *__restrict__ dst, const float *_
 
 // Observation header (smart_nanogrid_environment.py:199-240, central_management_system.py:53-60):
 // [solar(t), price(t), solar(t+1..t+3), price(t+1..t+3)] with PV, [price(t), price(t+1..t+3)] without.
-__device__ __forceinline__ void write_obs_header(float *o, const Params &p, const Tables *tb, int t, double ratio) {
+// irr / pn point at irr_norm[t] / price_norm[t] (the step kernel's LDS copy, or the tables).
+__device__ __forceinline__ void write_obs_header(float *o, const Params &p, const double *irr, const double *pn,
+                                                 double ratio) {
     int k = 0;
-    if (p.pv) o[k++] = (float)(tb->irr_norm[t] * ratio);
-    o[k++] = (float)tb->price_norm[t];
+    if (p.pv) o[k++] = (float)(irr[0] * ratio);
+    o[k++] = (float)pn[0];
     if (p.pv) {
 #pragma unroll
-        for (int j = 1; j <= 3; ++j) o[k++] = (float)(tb->irr_norm[t + j] * ratio);
+        for (int j = 1; j <= 3; ++j) o[k++] = (float)(irr[j] * ratio);
     }
 #pragma unroll
-    for (int j = 1; j <= 3; ++j) o[k++] = (float)tb->price_norm[t + j];
+    for (int j = 1; j <= 3; ++j) o[k++] = (float)pn[j];
+}
+
+// Per-step constants staged in LDS by the step kernel: irr_norm[t..t+3], price_norm[t..t+3],
+// pv_power[t], price[t].
+enum { CST_IRR = 0, CST_PN = 4, CST_PV = 8, CST_PRICE = 9, CST_COUNT = 10 };
+__device__ __forceinline__ double step_constant(const Tables *tb, int t, int i) {
+    return i < CST_PN ? tb->irr_norm[t + i]
+                      : i < CST_PV ? tb->price_norm[t + i - CST_PN] : i == CST_PV ? tb->pv_power[t] : tb->price[t];
 }
 
 // Remaining time to departure / 24 (smart_nanogrid_environment.py:216-217) as float32.
@@ -197,16 +207,19 @@ struct ChargerResult {
     double pw;      // charger power value (kW), f64 array element of charging_station.py:282
     double q;       // insufficient-charge penalty term (0 if not checked / not insufficient)
     double soc;     // SOC[c, t] after the step
-    double nonexist;
+    uint32_t nx;    // 1: non-zero action on an empty charger (100 penalty points, diagnostics only)
     uint32_t fl;
 };
 
 // Written with selects rather than branches so the chargers of an env interleave (ILP hides the
-// f64 latency at one wavefront per SIMD); only the inverted-flag discharge keeps a (divergent)
-// branch for its division when dt is not a power of two.  Occupied chargers have cap in [1, 255]
+// f64 latency at one wavefront per SIMD); the general variant keeps a (divergent) branch for the
+// inverted-flag discharge division when dt is not a power of two.  Occupied chargers have cap in [1, 255]
 // (validated when a scenario is encoded).
+// FAST (NumPy-2 promotion and dt a power of two, e.g. the 1 h default) is straight-line code, so the
+// compiler interleaves the chargers of an env.
+template <bool FAST>
 __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, double req,
-                                                      float a, int t, const double *__restrict__ s_rcp) {
+                                                      float a, int t, double rcap) {
     ChargerResult o;
     const double margin = 0.05 * req;
     const double d = (req - run) * 10;
@@ -214,35 +227,36 @@ __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t 
     o.q = insufficient ? d * d : 0.0;
 
     const bool occ = (w & W_OCC) != 0;
-    const double prev = (w & W_STATIC) ? aux : run;
+    // previous SoC of an occupied charger, or the recorded SOC[c, t] of an empty one
+    const double prev = (occ && !(w & W_STATIC)) ? run : aux;
     const uint32_t capi = (w >> W_CAP_SHIFT) & 0xffu;
     const double cap = (double)capi;
     const bool idle = (a == 0.0f);
     const bool chg = (a > 0.0f);
     double pc, change;
-    if (p.legacy) {   // NumPy < 2: float32 scalar * int -> float64 (float64 numerator: plain division)
+    if (!FAST && p.legacy) {   // NumPy < 2: float32 scalar * int -> float64 (float64 numerator: plain division)
         pc = ((double)a * p.ev_power) * p.ev_eff;
         change = (pc * p.dt) / cap;
     } else {          // NumPy 2 (NEP 50): float32 product
         const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
         const float pdt = __fmul_rn(pf, p.dt_f);
         pc = (double)pf;
-        change = div_by_cap((double)pdt, cap, s_rcp[capi]);
+        change = div_by_cap((double)pdt, cap, rcap);
     }
     const double calc = prev + change;
     double pw_dis = pc;                                          // inverted flag, charger.py:122-132
-    if (occ && !idle && !chg && calc >= 0.0) {
+    if (FAST) {
+        pw_dis = (calc >= 0.0) ? -((prev * cap) * p.rdt) : pc;
+    } else if (occ && !idle && !chg && calc >= 0.0) {
         const double x = prev * cap;
         pw_dis = -(p.dt_pow2 ? x * p.rdt : x / p.dt);
     }
     const double soc_chg = (1.0 < calc) ? 1.0 : calc;           // min(calc, 1.0)
     const double soc_dis = (calc > 0.0) ? calc : 0.0;           // max(0.0, calc)
-    const bool act = !idle && p.bounded;
-    const double nsoc = act ? (chg ? soc_chg : soc_dis) : prev;
-    const double pw = act ? (chg ? pc : pw_dis) : 0.0;          // full power billed when charging
-    o.soc = occ ? nsoc : aux;                                   // empty charger: SOC[c, t] as recorded
-    o.pw = occ ? pw : 0.0;
-    o.nonexist = (!occ && !idle) ? 100.0 : 0.0;
+    const bool moved = occ && !idle && p.bounded;
+    o.soc = moved ? (chg ? soc_chg : soc_dis) : prev;
+    o.pw = moved ? (chg ? pc : pw_dis) : 0.0;                   // full power billed when charging
+    o.nx = (!occ && !idle) ? 1u : 0u;
     o.fl = (occ && !idle && !p.bounded) ? (uint32_t)SNG_FLAG_CHARGING_MODE : 0u;
     return o;
 }
@@ -256,16 +270,20 @@ template <bool DIAG>
 __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, const InfoPtrs &info, int64_t e,
                                          int t, double ratio, double bess, float bess_action, double p_ch,
                                          double p_dis, double pen_v, double nonexist, uint32_t fl, float *o_row,
-                                         double *__restrict__ reward, uint8_t *__restrict__ done) {
-    const Tables *tb = s.tables;
-    const double solar = p.pv ? tb->pv_power[t] * ratio : 0.0;   // central_management_system.py:99-103
+                                         const double *cst, double ret_prev, double bess0, double *__restrict__ reward,
+                                         uint8_t *__restrict__ done) {
+    // no global loads in here: a load would wait (vmcnt) for every SoC store the env just issued
+    const double solar = p.pv ? cst[CST_PV] * ratio : 0.0;         // central_management_system.py:99-103
     const double demand = p_ch + p_dis;                            // :105
     if (demand < 0.0) fl |= p.v2x ? SNG_FLAG_V2X_BREAKPOINT : SNG_FLAG_NEGATIVE_DEMAND;
     double rem = demand - solar;                                   // :167
 
     double pen_b = 0.0, bpow = 0.0, bcalc = 0.0;
     if (p.bess) {
-        if (t == 0) s.bess0[e] = bess;                             // :93-94
+        if (t == 0) {                                              // :93-94
+            s.bess0[e] = bess;
+            bess0 = bess;
+        }
         const double ba = (double)bess_action;
         if (ba == 0.0) {
             bpow = 0.0;
@@ -300,19 +318,19 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
 
     const double grid = rem;
     const double energy = grid * p.dt;
-    const double price = tb->price[t];
+    const double price = cst[CST_PRICE];
     const double cost = (energy < 0.0) ? (energy * p.sell_coef) * price : energy * price;
     const double tot_pen = p.bat_pen_w * pen_b + pen_v;
     const double total = p.grid_w * fabs(cost) + tot_pen;
     reward[e] = -total;
     done[e] = (t + 1 == p.T) ? 1 : 0;
 
-    write_obs_header(o_row, p, tb, t, ratio);
+    write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio);
     if (p.bess) o_row[p.obs_dim - 1] = (float)bess;
 
-    if (fl) s.flags[e] |= fl;
+    if (fl) atomicOr(&s.flags[e], fl);   // rare (sticky error bits); no-return atomic, nothing waits
     if (info.flags) info.flags[e] = fl;
-    if (info.episode_return) info.episode_return[e] += -total;
+    if (info.episode_return) info.episode_return[e] = ret_prev + -total;
     if (DIAG) {
         if (info.grid_power) info.grid_power[e] = grid;
         if (info.p_charge) info.p_charge[e] = p_ch;
@@ -326,7 +344,7 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
         if (info.bess_power) info.bess_power[e] = bpow;
         if (info.bess_calc_power) info.bess_calc_power[e] = bcalc;
         if (info.nonexistent) info.nonexistent[e] = nonexist;
-        if (info.bess_initial) info.bess_initial[e] = p.bess ? s.bess0[e] : 0.0;
+        if (info.bess_initial) info.bess_initial[e] = p.bess ? bess0 : 0.0;
     }
 }
 
@@ -336,7 +354,7 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
 __host__ __device__ constexpr int step_block(int NC) { return (NC > 0 && NC <= 16) ? 256 : 64; }
 
 // LDS carve-up of the step kernel (every region 16-byte aligned):
-//   act [ENVS][A] f32 | obs [ENVS][O] f32 | rcp [256] f64 | pos [ENVS][NC] f64 | neg [ENVS][NC] f64
+//   act [ENVS][A] f32 | obs [ENVS][O] f32 | rcp [256] f64 | cst [16] f64 | pos [ENVS][NC] f64 | neg [ENVS][NC] f64
 //   | (L > 1) pw [ENVS][NC] f64 | q [ENVS][NC] f64
 template <int NC, int L>
 struct StepLds {
@@ -346,7 +364,7 @@ struct StepLds {
     __host__ __device__ static int act_floats(int A) { return round4(ENVS * A); }
     __host__ __device__ static int obs_floats(int O) { return round4(ENVS * O); }
     __host__ __device__ static size_t bytes(int A, int O) {
-        size_t b = (size_t)(act_floats(A) + obs_floats(O)) * 4 + 256 * 8;
+        size_t b = (size_t)(act_floats(A) + obs_floats(O)) * 4 + (256 + 16) * 8;
         if (kRows) b += (size_t)2 * ENVS * NC * 8;
         if (L > 1) b += (size_t)2 * ENVS * NC * 8;
         return b;
@@ -361,7 +379,7 @@ struct StepLds {
 // Every per-charger load of a lane's batch is issued before any of it is used, and the first
 // batch before the action staging wait, so one lane keeps 3*CH + 2 requests in flight.
 // ---------------------------------------------------------------------------------
-template <int NC, int L, bool DIAG>
+template <int NC, int L, bool DIAG, bool FAST>
 __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceState s, InfoPtrs info,
                                                               const float *__restrict__ act, float *__restrict__ obs,
                                                               double *__restrict__ reward, uint8_t *__restrict__ done,
@@ -385,7 +403,8 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     float *s_act = lds;
     float *s_obs = lds + Lay::act_floats(A);
     double *s_rcp = reinterpret_cast<double *>(s_obs + Lay::obs_floats(O));
-    double *s_pos = s_rcp + 256;                                  // [ENVS][NC] compacted positive powers
+    double *s_cst = s_rcp + 256;                                  // [16] per-step constants (CST_*)
+    double *s_pos = s_cst + 16;                                   // [ENVS][NC] compacted positive powers
     double *s_neg = s_pos + (kRows ? ENVS * NC : 0);              // [ENVS][NC] compacted negative powers
     double *s_pw = s_neg + (kRows ? ENVS * NC : 0);               // [ENVS][NC] per-charger powers (L > 1)
     double *s_q = s_pw + (L > 1 ? ENVS * NC : 0);                 // [ENVS][NC] per-charger penalty terms
@@ -408,16 +427,31 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                 w[j] = word[idx];
                 aux[j] = auxv[idx];
                 run[j] = socv[(size_t)c * E + e];
-                req[j] = p.req_stream ? reqv[idx] : 1.0;
+            } else {
+                w[j] = 0u;
+                aux[j] = run[j] = 0.0;
             }
+        }
+        if (p.req_stream) {
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int c = c0 + j;
+                req[j] = (c < cend) ? reqv[(tbase + c) * (size_t)E + e] : 1.0;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < CH; ++j) req[j] = 1.0;
         }
     };
 
-    double ratio = 0.0, bess = 0.0;
+    double ratio = 0.0, bess = 0.0, pen0 = 0.0, ret_prev = 0.0, bess0 = 0.0;
     if (live) {
         if (leader) {
             ratio = s.ratio[e];
             if (p.bess) bess = s.bess[e];
+            if (t == 0) pen0 = s.pen0[e];
+            if (info.episode_return) ret_prev = info.episode_return[e];
+            if (DIAG && p.bess && t > 0 && info.bess_initial) bess0 = s.bess0[e];
         }
         load_batch(cbeg);
     }
@@ -426,6 +460,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
 #endif
 #pragma unroll
     for (int i = tid; i < 256; i += BLOCK) s_rcp[i] = s.tables->recip[i];
+    if (tid < CST_COUNT) s_cst[tid] = step_constant(s.tables, t, tid);
     copy_in<(NC > 0 && NC < 16) ? 4 : 8, BLOCK>(s_act, act + e0 * A, nblk * A, vec_io != 0, tid);
     __syncthreads();
     SNG_STAMP(1);
@@ -449,8 +484,11 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             const bool ip = pw > 0.0, in = pw < 0.0;
             row_pos[n_pos] = pw;
             row_neg[n_neg] = pw;
-            seq_pos = ip ? seq_pos + pw : seq_pos;
-            seq_neg = in ? seq_neg + pw : seq_neg;
+            // + max(pw, 0) / + min(pw, 0): adds the kept element, or a zero that leaves the running
+            // sum exactly unchanged (v_max/v_min return the non-NaN operand: a NaN power is
+            // dropped, as numpy's P[P > 0] drops it)
+            seq_pos += __builtin_fmax(pw, 0.0);
+            seq_neg += __builtin_fmin(pw, 0.0);
             n_pos += ip ? 1 : 0;
             n_neg += in ? 1 : 0;
         } else {
@@ -458,20 +496,31 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             if (pw < 0.0) neg.push(pw);
         }
     };
-    double pen_v = 0.0, nonexist = 0.0;
+    double pen_v = 0.0;
+    uint32_t n_nonexist = 0;
     uint32_t fl = 0;
     if (live) {
         for (int c0 = cbeg; c0 < cend; c0 += CH) {
             if (c0 != cbeg) load_batch(c0);
+            // all LDS reads of the batch (actions, 1/cap) ahead of the LDS writes below, so they
+            // issue back to back and the chargers' arithmetic interleaves
+            float av[CH];
+            double rc[CH];
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int c = c0 + j;
+                av[j] = (c < cend) ? a_row[c] : 0.0f;
+                rc[j] = s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu];
+            }
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
                 if (c >= cend) break;
-                const ChargerResult r = charger_step(p, w[j], aux[j], run[j], req[j], a_row[c], t, s_rcp);
+                const ChargerResult r = charger_step<FAST>(p, w[j], aux[j], run[j], req[j], av[j], t, rc[j]);
                 socv[(size_t)c * E + e] = r.soc;
                 o_row[k_soc + c] = (float)r.soc;
                 o_row[k_soc + n + c] = departure_obs(w[j]);
-                nonexist += r.nonexist;
+                n_nonexist += r.nx;
                 fl |= r.fl;
                 if (L == 1) {
                     pen_v += r.q;
@@ -484,11 +533,11 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         }
     }
     if (L > 1) {
-        // gather the env's lanes: exact sums (multiples of 100) and flag bits, then in-order
+        // gather the env's lanes: counts and flag bits, then in-order
         // penalty / power sums by the leader from LDS
 #pragma unroll
         for (int off = 1; off < L; off <<= 1) {
-            nonexist += __shfl_down(nonexist, off, L);
+            n_nonexist += (uint32_t)__shfl_down((int)n_nonexist, off, L);
             fl |= (uint32_t)__shfl_down((int)fl, off, L);
         }
         __syncthreads();
@@ -501,7 +550,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         }
     }
     if (live && leader) {
-        if (t == 0) pen_v = s.pen0[e];
+        // t = 0 reads the python index -1 slot (pen0); every per-charger term is 0 there, and
+        // adding +0.0 / adding to +0.0 is exact, so this equals the reference's choice of sum
+        pen_v += pen0;
         double p_ch, p_dis;
         if (kRows) {
             p_ch = pairwise_row(row_pos, n_pos, seq_pos);
@@ -510,8 +561,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             p_ch = pos.result();
             p_dis = neg.result();
         }
-        env_tail<DIAG>(p, s, info, e, t, ratio, bess, p.bess ? a_row[n] : 0.0f, p_ch, p_dis, pen_v, nonexist, fl,
-                       o_row, reward, done);
+        env_tail<DIAG>(p, s, info, e, t, ratio, bess, p.bess ? a_row[n] : 0.0f, p_ch, p_dis, pen_v,
+                       100.0 * (double)n_nonexist, fl,
+                       o_row, s_cst, ret_prev, bess0, reward, done);
     }
     __syncthreads();
     SNG_STAMP(2);
@@ -535,7 +587,7 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
     float *o_row = lds + tid * O;
     if (tid < nblk) {
         const double ratio = s.ratio[e];
-        write_obs_header(o_row, p, s.tables, 0, ratio);
+        write_obs_header(o_row, p, s.tables->irr_norm, s.tables->price_norm, ratio);
         const int k = p.pv ? 8 : 4;
         for (int c = 0; c < n; ++c) {
             const size_t idx = (size_t)c * E + e;   // t = 0 slice
@@ -662,12 +714,12 @@ static void launch_step_t(const Params &p, const DeviceState &s, const InfoPtrs 
     using Lay = StepLds<NC, L>;
     const dim3 grid((unsigned)((E + Lay::ENVS - 1) / Lay::ENVS)), block(Lay::BLOCK);
     const uint32_t lds = (uint32_t)Lay::bytes(p.act_dim, p.obs_dim);
+    auto kern = (!p.legacy && p.dt_pow2) ? step_kernel<NC, L, DIAG, true> : step_kernel<NC, L, DIAG, false>;
     if (ev)
-        hipExtLaunchKernelGGL((step_kernel<NC, L, DIAG>), grid, block, lds, stream, ev->start, ev->stop, 0u, p, s, info,
-                              act, obs, reward, done, E, t, vec_io);
+        hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, p, s, info, act, obs, reward,
+                              done, E, t, vec_io);
     else
-        hipLaunchKernelGGL((step_kernel<NC, L, DIAG>), grid, block, lds, stream, p, s, info, act, obs, reward, done, E,
-                           t, vec_io);
+        hipLaunchKernelGGL(kern, grid, block, lds, stream, p, s, info, act, obs, reward, done, E, t, vec_io);
 }
 
 template <int NC, bool DIAG>
