@@ -27,6 +27,26 @@ namespace sng {
 
 constexpr int kWave = 64;
 
+// Streaming (nontemporal) stores for the step's bulk outputs (SoC, observations): they leave
+// less dirty L2 for the end-of-kernel release (measured 8.92 -> 8.17 us per step at 65,536 x 10).
+#define SNG_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
+// Streaming loads for the scenario timeline (read once per day): experiment switch.
+#ifdef SNG_NT_LOADS
+#define SNG_LD(src) __builtin_nontemporal_load(&(src))
+#else
+#define SNG_LD(src) (src)
+#endif
+#ifdef SNG_NT_GEN
+#define SNG_GST(dst, v) __builtin_nontemporal_store((v), &(dst))
+#else
+#define SNG_GST(dst, v) ((dst) = (v))
+#endif
+#ifdef SNG_NT_LOADS_SOC
+#define SNG_LDS(src) __builtin_nontemporal_load(&(src))
+#else
+#define SNG_LDS(src) (src)
+#endif
+
 #ifdef SNG_STAMPS
 // Diagnostic build only (make stamps): per-workgroup s_memrealtime stamps (100 MHz) at the
 // phase boundaries of the step kernel -> g_stamps[block*4 + k].  Never compiled into libsng.so.
@@ -144,9 +164,10 @@ template <int BLOCK>
 __device__ __forceinline__ void copy_out(float *__restrict__ dst, const float *__restrict__ src, int count,
                                          bool vec, int tid) {
     if (vec && (count & 3) == 0) {
-        const float4 *s4 = reinterpret_cast<const float4 *>(src);
-        float4 *d4 = reinterpret_cast<float4 *>(dst);
-        for (int i = tid; i < (count >> 2); i += BLOCK) d4[i] = s4[i];
+        typedef float v4f __attribute__((ext_vector_type(4)));
+        const v4f *s4 = reinterpret_cast<const v4f *>(src);
+        v4f *d4 = reinterpret_cast<v4f *>(dst);
+        for (int i = tid; i < (count >> 2); i += BLOCK) SNG_ST(d4[i], s4[i]);
     } else {
         for (int i = tid; i < count; i += BLOCK) dst[i] = src[i];
     }
@@ -221,6 +242,15 @@ template <bool FAST>
 __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, double req,
                                                       float a, int t, double rcap) {
     ChargerResult o;
+#ifdef SNG_MEMFLOOR
+    // diagnostic build only (make memfloor): same loads and stores, trivial arithmetic
+    o.q = 0.0;
+    o.pw = aux + (double)a;
+    o.soc = run + aux;
+    o.nx = 0u;
+    o.fl = 0u;
+    return o;
+#endif
     const double margin = 0.05 * req;
     const double d = (req - run) * 10;
     const bool insufficient = (t > 0) && (w & W_PEN) && (run < req - margin);
@@ -313,7 +343,7 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
         } else if (!(bess <= 1.0)) {
             fl |= SNG_FLAG_BESS_SOC_ABOVE_1;
         }
-        s.bess[e] = bess;
+        SNG_ST(s.bess[e], bess);
     }
 
     const double grid = rem;
@@ -322,15 +352,15 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     const double cost = (energy < 0.0) ? (energy * p.sell_coef) * price : energy * price;
     const double tot_pen = p.bat_pen_w * pen_b + pen_v;
     const double total = p.grid_w * fabs(cost) + tot_pen;
-    reward[e] = -total;
-    done[e] = (t + 1 == p.T) ? 1 : 0;
+    SNG_ST(reward[e], -total);
+    SNG_ST(done[e], (uint8_t)((t + 1 == p.T) ? 1 : 0));
 
     write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio);
     if (p.bess) o_row[p.obs_dim - 1] = (float)bess;
 
     if (fl) atomicOr(&s.flags[e], fl);   // rare (sticky error bits); no-return atomic, nothing waits
     if (info.flags) info.flags[e] = fl;
-    if (info.episode_return) info.episode_return[e] = ret_prev + -total;
+    if (info.episode_return) SNG_ST(info.episode_return[e], ret_prev + -total);
     if (DIAG) {
         if (info.grid_power) info.grid_power[e] = grid;
         if (info.p_charge) info.p_charge[e] = p_ch;
@@ -424,9 +454,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             const int c = c0 + j;
             if (c < cend) {
                 const size_t idx = (tbase + c) * (size_t)E + e;
-                w[j] = word[idx];
-                aux[j] = auxv[idx];
-                run[j] = socv[(size_t)c * E + e];
+                w[j] = SNG_LD(word[idx]);
+                aux[j] = SNG_LD(auxv[idx]);
+                run[j] = SNG_LDS(socv[(size_t)c * E + e]);
             } else {
                 w[j] = 0u;
                 aux[j] = run[j] = 0.0;
@@ -517,7 +547,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                 const int c = c0 + j;
                 if (c >= cend) break;
                 const ChargerResult r = charger_step<FAST>(p, w[j], aux[j], run[j], req[j], av[j], t, rc[j]);
-                socv[(size_t)c * E + e] = r.soc;
+                SNG_ST(socv[(size_t)c * E + e], r.soc);
                 o_row[k_soc + c] = (float)r.soc;
                 o_row[k_soc + n + c] = departure_obs(w[j]);
                 n_nonexist += r.nx;
@@ -685,9 +715,9 @@ __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s
         }
         const int rem = occ ? dep - t : 0;
         const size_t idx = ((size_t)t * n + c) * (size_t)E + e;
-        s.word[idx] = pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem);
-        s.aux[idx] = arrived ? soc_arr : 0.0;   // dense: full-line stores
-        if (p.req_stream) s.req[idx] = pen ? req : 0.0;
+        SNG_GST(s.word[idx], pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem));
+        SNG_GST(s.aux[idx], arrived ? soc_arr : 0.0);   // dense: full-line stores
+        if (p.req_stream) SNG_GST(s.req[idx], pen ? req : 0.0);
         prev_occ = occ;
         prev_rem = rem;
     }
