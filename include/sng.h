@@ -56,7 +56,7 @@ typedef enum SngRngMode {
      * reference's reset()/step() sequence (charging_station.py:200-279,
      * smart_nanogrid_environment.py:190,358).  Generated on the host CPU threads. */
     SNG_RNG_REFERENCE = 0,
-    /* Counter-based Philox streams on the GPU: same distributions, different draws.
+    /* Counter-based hash streams on the GPU: same distributions, different draws.
      * Fully device-resident; graph-capturable. */
     SNG_RNG_DEVICE = 1
 } SngRngMode;
@@ -169,7 +169,7 @@ int sng_get_timestep(const SngEnv *env);
 
 /* Global index of this handle's env 0 when one population of envs is sharded over several
  * GPUs/processes: env i then draws the streams of global env offset+i (reference RNG:
- * seed + offset + i; device RNG: Philox counter offset + i), so a sharded run reproduces the
+ * seed + offset + i; device RNG: hash-stream key of global env offset + i), so a sharded run reproduces the
  * single-GPU run bit for bit.  Call before reset. */
 int sng_set_env_offset(SngEnv *env, int64_t offset);
 

@@ -638,24 +638,35 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
 // Device RNG day generator: the reference's per-charger vehicle process
 // (charging_station.py:200-279: arrival with p = 0.4 when the charger is free, arrival SoC
 // U(0.1, 0.9), capacity U{15..119}, requested SoC, departure U{t+4/dt .. min(t+10/dt, T+1/dt)-1})
-// with counter-based SplitMix64 streams, one per (global env, charger, day).
+// with counter-based 32-bit hash streams, one per (global env, charger, day): draw i of a
+// stream is mix32(key + i * golden), three 32-bit multiplies (the earlier 64-bit SplitMix
+// streams cost ~4x the VALU; the kernel is bound by its dense timeline stores otherwise).
 // Thread = (env, charger); writes the dense word / aux (/ req) timeline.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
-    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
-    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
-    return z ^ (z >> 31);
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {   // "triple32" integer hash (bijective)
+    x ^= x >> 17;
+    x *= 0xed5ad4bbu;
+    x ^= x >> 11;
+    x *= 0xac4c1b51u;
+    x ^= x >> 15;
+    x *= 0x31848babu;
+    x ^= x >> 14;
+    return x;
 }
 
-struct SplitMix {
-    uint64_t state;
-    __device__ __forceinline__ uint64_t next() {
-        state += 0x9e3779b97f4a7c15ull;
-        return splitmix64(state);
-    }
+struct HashStream {
+    uint32_t key, ctr;
+    __device__ __forceinline__ uint32_t next() { return mix32(key + (ctr++) * 0x9e3779b9u); }
 };
 
-__device__ __forceinline__ double u53(uint64_t x) { return (double)(x >> 11) * 0x1.0p-53; }
+__device__ __forceinline__ double u32_unit(uint32_t x) { return (double)x * 0x1.0p-32; }   // [0, 1)
+
+// Stream key of (seed, global env, charger | domain, day).
+__device__ __forceinline__ uint32_t stream_key(uint64_t seed, uint64_t ge, uint32_t lane, uint64_t day) {
+    const uint32_t k0 = mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + (uint32_t)day * 0x9e3779b9u));
+    const uint32_t k1 = mix32(k0 ^ (uint32_t)ge);
+    return mix32(k1 ^ ((uint32_t)(ge >> 32) * 0x85ebca6bu + lane * 0xc2b2ae35u + 0x27d4eb2fu));
+}
 
 __device__ __forceinline__ int below(uint32_t x, int n) {   // floor(x * n / 2^32)
     return (int)(((uint64_t)x * (uint64_t)n) >> 32);
@@ -664,14 +675,16 @@ __device__ __forceinline__ int below(uint32_t x, int n) {   // floor(x * n / 2^3
 // round(rand() - 0.1) == 1  <=>  rand() > 0.6: the 32-bit threshold ceil(0.6 * 2^32)
 constexpr uint32_t kArrivalThreshold = 2576980378u;
 
-__global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
-                                                         int i4, int i10, int i1) {
-    const int64_t e = (int64_t)blockIdx.x * kWave + threadIdx.x;
+constexpr int kGenBlock = 256;   // 4 waves of consecutive envs, same charger
+
+__global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
+                                                             int i4, int i10, int i1) {
+    const int64_t e = (int64_t)blockIdx.x * kGenBlock + threadIdx.x;
     const int c = blockIdx.y;
     if (e >= E) return;
     const uint64_t day = *s.episode;
     const uint64_t ge = (uint64_t)(e + p.env_offset);   // global env id
-    SplitMix rng{splitmix64(splitmix64(splitmix64(seed ^ 0x5ee6c0deull) ^ ge) ^ ((uint64_t)c << 32 | (day & 0xffffffffull)))};
+    HashStream rng{stream_key(seed, ge, (uint32_t)c, day), 0u};
     const int T = p.T, n = p.n;
 
     bool present = false, prev_occ = false;
@@ -682,20 +695,19 @@ __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s
         bool arrived = false;
         double soc_arr = 0.0;
         if (!present) {
-            const uint64_t x = rng.next();
-            if ((uint32_t)(x >> 32) >= kArrivalThreshold) {
+            if (rng.next() >= kArrivalThreshold) {
                 arrived = true;
                 present = true;
-                soc_arr = 0.1 + (0.9 - 0.1) * u53(rng.next());            // uniform(0.1, 0.9)
-                const uint64_t y = rng.next();
-                cap = p.diff_caps ? (uint32_t)(15 + below((uint32_t)(y >> 32), 105)) : 40u;   // randint(15, 120)
+                soc_arr = 0.1 + (0.9 - 0.1) * u32_unit(rng.next());       // uniform(0.1, 0.9)
+                const uint32_t y = rng.next();
+                cap = p.diff_caps ? (uint32_t)(15 + below(y, 105)) : 40u;   // randint(15, 120)
                 const int hi_c = t + i10, hi_d = T + i1;
                 const int high = hi_c < hi_d ? hi_c : hi_d;
                 const int low = t + i4;
-                dep = (low >= high) ? low : low + below((uint32_t)y, high - low);
+                dep = (low >= high) ? low : low + below(rng.next(), high - low);
                 if (p.req_enabled) {
                     const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
-                    req = lo + (1.0 - lo) * u53(rng.next());
+                    req = lo + (1.0 - lo) * u32_unit(rng.next());
                 } else {
                     req = 1.0;
                 }
@@ -722,8 +734,8 @@ __global__ __launch_bounds__(kWave) void generate_kernel(Params p, DeviceState s
         prev_rem = rem;
     }
     if (c == 0) {
-        SplitMix r2{splitmix64(splitmix64(seed ^ 0x7a71'0000ull) ^ ge ^ (day << 40))};
-        s.ratio[e] = (double)below((uint32_t)(r2.next() >> 32), 181) / 100;   // random.randint(0, 180) / 100
+        HashStream r2{stream_key(seed, ge, 0x7a710000u, day), 0u};            // the PV-ratio domain
+        s.ratio[e] = (double)below(r2.next(), 181) / 100;   // random.randint(0, 180) / 100
         s.pen0[e] = 0.0;
     }
 }
@@ -821,7 +833,7 @@ hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, do
 
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            hipStream_t stream) {
-    const dim3 grid((unsigned)((E + kWave - 1) / kWave), (unsigned)p.n), block(kWave);
+    const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)p.n), block(kGenBlock);
     hipLaunchKernelGGL(generate_kernel, grid, block, 0, stream, p, s, seed, E, i4, i10, i1);
     return hipGetLastError();
 }

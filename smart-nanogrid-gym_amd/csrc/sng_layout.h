@@ -84,7 +84,7 @@ struct DeviceState {
     uint32_t *word;
     double *aux, *req;
     uint32_t *flags;
-    uint64_t *episode;        // device-side day counter for the Philox generator
+    uint64_t *episode;        // device-side day counter for the device generator
     const Tables *tables;
 };
 

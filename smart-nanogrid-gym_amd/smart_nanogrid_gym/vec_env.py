@@ -40,7 +40,7 @@ class SmartNanogridVecEnv:
     Parameters (besides the reference's own keyword arguments):
       seed   -- env i behaves like the reference after `np.random.seed(seed + i); random.seed(seed + i)`
       device -- HIP device index
-      rng    -- 'reference' (host MT19937 streams, reference-exact days) or 'device' (Philox on the GPU)
+      rng    -- 'reference' (host MT19937 streams, reference-exact days) or 'device' (counter-based hash streams on the GPU)
       info   -- True: also fill the per-step diagnostics (grid power, BESS SoC, penalties ...)
       env_offset -- global index of env 0 when one env population is sharded over GPUs
                     (parallel.shard_envs); env i then behaves as global env env_offset + i

@@ -174,7 +174,7 @@ def test_full_size_sampled_parity_65536():
 
 
 def test_device_rng_day_distribution_and_invariants():
-    """GPU Philox days: same distributions as the reference generator (oracle MT draws)."""
+    """Device-generator days: same distributions as the reference generator (oracle MT draws)."""
     E, N = 65536, 10
     kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
               vehicle_uncharged_penalty_mode="sparse")
