@@ -61,14 +61,15 @@ def cpu_baseline(chargers, budget_s):
                       f"C oracle (scalar restatement of the reference) on 1 host thread, {dt:.1f} s"}
 
 
-def load_pmc_traffic(n_envs, chargers):
-    """Per-launch HBM bytes of the step kernel from the committed rocprofv3 PMC summary."""
+def load_pmc_traffic(n_envs, chargers, kernel):
+    """Per-launch HBM bytes of the step kernel from the committed rocprofv3 PMC summary
+    (only when it was collected for this kernel instantiation and size)."""
     path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
     if not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
-        if d.get("envs") == n_envs and d.get("chargers") == chargers:
+        if d.get("envs") == n_envs and d.get("chargers") == chargers and d.get("kernel") == kernel:
             return d.get("bytes_per_launch")
     except Exception:
         return None
@@ -157,9 +158,10 @@ def main():
         launch_s = float(np.mean(kernel_ms)) / 1e3
         bpl = step_kernel_bytes(N) * E
         achieved = bpl / launch_s / 1e9
+        kernel = f"void sng::step_kernel<{N}, {venv.step_lanes}, false, true>"
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N),
-                "kernel": "sng::step_kernel<10>", "bytes_per_launch": bpl,
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N, kernel),
+                "kernel": kernel, "bytes_per_launch": bpl,
                 "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src}
         cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_budget)
         out = {"metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,

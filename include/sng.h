@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 1
+#define SNG_ABI_VERSION 2
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -110,6 +110,8 @@ typedef struct SngDims {
     int32_t timesteps;      /* 24 / dt */
     int32_t number_of_chargers;
     int64_t num_envs;
+    int32_t step_lanes_per_env;   /* lanes per env the step kernel runs with (SngConfig 0 = default) */
+    int32_t reserved;
 } SngDims;
 
 /* Optional per-step diagnostics: device pointers, each [num_envs]; NULL = not written.

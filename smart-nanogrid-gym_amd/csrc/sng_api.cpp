@@ -651,6 +651,8 @@ int sng_get_dims(const SngEnv *env, SngDims *out) {
     out->timesteps = env->p.T;
     out->number_of_chargers = env->p.n;
     out->num_envs = env->E;
+    out->step_lanes_per_env = env->p.lanes;
+    out->reserved = 0;
     return SNG_OK;
 }
 

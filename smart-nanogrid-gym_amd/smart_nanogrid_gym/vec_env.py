@@ -67,6 +67,7 @@ class SmartNanogridVecEnv:
         dims = _native.SngDims()
         check(lib().sng_get_dims(h, ctypes.byref(dims)), h)
         self.obs_dim, self.act_dim, self.timesteps = dims.obs_dim, dims.act_dim, dims.timesteps
+        self.step_lanes = dims.step_lanes_per_env
         E = self.num_envs
         dev = self.device
         self.actions_d = torch.zeros((E, self.act_dim), dtype=torch.float32, device=dev)
