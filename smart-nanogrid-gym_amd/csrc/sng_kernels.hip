@@ -160,6 +160,63 @@ __device__ __forceinline__ void copy_in(float *__restrict__ dst, const float *__
     }
 }
 
+// The same copy split in two so other loads can be issued in between: issue() puts the
+// block's tile in registers (one load per lane and k), commit() writes it to LDS.  When the
+// tile does not fit one round (count > 4 * K * BLOCK floats) issue() does nothing and commit()
+// falls back to copy_in.  Native vector types only (HIP's float4 wrapper keeps the array
+// from being promoted to registers).
+template <int K, int BLOCK>
+struct TileStage {
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    v4f v[K];
+    const float *src;
+    int count;
+    bool vec, one_round;
+    __device__ __forceinline__ void issue(const float *__restrict__ s, int cnt, bool vec_io, int tid) {
+        src = s;
+        count = cnt;
+        vec = vec_io && (cnt & 3) == 0;
+        one_round = vec ? (cnt >> 2) <= K * BLOCK : cnt <= K * BLOCK;
+        if (!one_round) return;
+        if (vec) {
+            const v4f *s4 = reinterpret_cast<const v4f *>(s);
+            const int n4 = cnt >> 2;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int i = k * BLOCK + tid;
+                v[k] = s4[i < n4 ? i : n4 - 1];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int i = k * BLOCK + tid;
+                v[k].x = s[i < cnt ? i : cnt - 1];
+            }
+        }
+    }
+    __device__ __forceinline__ void commit(float *__restrict__ dst, int tid) {
+        if (!one_round) {
+            copy_in<K, BLOCK>(dst, src, count, vec, tid);
+            return;
+        }
+        if (vec) {
+            v4f *d4 = reinterpret_cast<v4f *>(dst);
+            const int n4 = count >> 2;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {   // out-of-range threads rewrite the last element (same value)
+                const int i = k * BLOCK + tid;
+                d4[i < n4 ? i : n4 - 1] = v[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int i = k * BLOCK + tid;
+                dst[i < count ? i : count - 1] = v[k].x;
+            }
+        }
+    }
+};
+
 template <int BLOCK>
 __device__ __forceinline__ void copy_out(float *__restrict__ dst, const float *__restrict__ src, int count,
                                          bool vec, int tid) {
@@ -446,52 +503,74 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     const int cbeg = (L > 1) ? part * CH : 0;
     const int cend = (L > 1) ? ((cbeg + CH) < n ? (cbeg + CH) : n) : n;
 
+    // Loads are issued oldest-needed-last: everything the block barrier waits for (tables,
+    // actions tile) is issued after the conditional loads and before the per-charger state, and
+    // no branch separates it from the per-charger loads, so the wait before the LDS commits is
+    // vmcnt(#per-charger loads) and charger c's update starts as soon as its own loads land.
+    // Non-live lanes load a valid env (E - 1) and discard it.
+    const int64_t el = live ? e : E - 1;
     uint32_t w[CH];
     double aux[CH], run[CH], req[CH];
-    auto load_batch = [&](int c0) {
+    auto load_state = [&](int c0) {
 #pragma unroll
         for (int j = 0; j < CH; ++j) {
             const int c = c0 + j;
             if (c < cend) {
-                const size_t idx = (tbase + c) * (size_t)E + e;
+                const size_t idx = (tbase + c) * (size_t)E + el;
                 w[j] = SNG_LD(word[idx]);
                 aux[j] = SNG_LD(auxv[idx]);
-                run[j] = SNG_LDS(socv[(size_t)c * E + e]);
+                run[j] = SNG_LDS(socv[(size_t)c * E + el]);
             } else {
                 w[j] = 0u;
                 aux[j] = run[j] = 0.0;
             }
         }
+    };
+    auto load_req = [&](int c0) {
         if (p.req_stream) {
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
-                req[j] = (c < cend) ? reqv[(tbase + c) * (size_t)E + e] : 1.0;
+                req[j] = (c < cend) ? reqv[(tbase + c) * (size_t)E + el] : 1.0;
             }
         } else {
 #pragma unroll
             for (int j = 0; j < CH; ++j) req[j] = 1.0;
         }
     };
+    auto load_batch = [&](int c0) {
+        load_req(c0);
+        load_state(c0);
+    };
 
-    double ratio = 0.0, bess = 0.0, pen0 = 0.0, ret_prev = 0.0, bess0 = 0.0;
-    if (live) {
-        if (leader) {
-            ratio = s.ratio[e];
-            if (p.bess) bess = s.bess[e];
-            if (t == 0) pen0 = s.pen0[e];
-            if (info.episode_return) ret_prev = info.episode_return[e];
-            if (DIAG && p.bess && t > 0 && info.bess_initial) bess0 = s.bess0[e];
-        }
-        load_batch(cbeg);
-    }
+    // 1. per-env values: pointer selects rather than branches (a disabled stream re-reads ratio)
+    const double ratio = s.ratio[el];
+    const double bess_l = (p.bess ? s.bess : s.ratio)[el];
+    const double pen0_l = (t == 0 ? s.pen0 : s.ratio)[el];
+    const double ret_l = (info.episode_return ? info.episode_return : s.ratio)[el];
+    const double bess0 = DIAG ? ((p.bess && t > 0 && info.bess_initial) ? s.bess0 : s.ratio)[el] : 0.0;
+    const double bess = p.bess ? bess_l : 0.0;
+    const double pen0 = (t == 0) ? pen0_l : 0.0;
+    const double ret_prev = info.episode_return ? ret_l : 0.0;
+    // 2. requested SoC of the first batch (uniform branch, ahead of the tile)
+    load_req(cbeg);
+    // 3. tables and the actions tile
+    constexpr int RCP_PER_THREAD = 256 / BLOCK;
+    double rcp_v[RCP_PER_THREAD];
+#pragma unroll
+    for (int k = 0; k < RCP_PER_THREAD; ++k) rcp_v[k] = s.tables->recip[k * BLOCK + tid];
+    const double cst_v = (tid < CST_COUNT) ? step_constant(s.tables, t, tid) : 0.0;
+    TileStage<(NC > 0 && NC < 16) ? 4 : 8, BLOCK> act_tile;
+    act_tile.issue(act + e0 * A, nblk * A, vec_io != 0, tid);
+    // 4. per-charger state of the first batch
+    load_state(cbeg);
 #ifdef SNG_STAMPS
     if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
 #endif
 #pragma unroll
-    for (int i = tid; i < 256; i += BLOCK) s_rcp[i] = s.tables->recip[i];
-    if (tid < CST_COUNT) s_cst[tid] = step_constant(s.tables, t, tid);
-    copy_in<(NC > 0 && NC < 16) ? 4 : 8, BLOCK>(s_act, act + e0 * A, nblk * A, vec_io != 0, tid);
+    for (int k = 0; k < RCP_PER_THREAD; ++k) s_rcp[k * BLOCK + tid] = rcp_v[k];
+    if (tid < CST_COUNT) s_cst[tid] = cst_v;
+    act_tile.commit(s_act, tid);
     __syncthreads();
     SNG_STAMP(1);
 
