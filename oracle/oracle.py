@@ -37,7 +37,10 @@ def lib():
         dp, fp, ip = (ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_float),
                       ctypes.POINTER(ctypes.c_int))
         L.orc_cfg_new.restype = vp
-        L.orc_cfg_new.argtypes = [i, d, i, i, i, i, i, i, i, i, d, i, dp, ctypes.c_long]
+        L.orc_cfg_new.argtypes = [i, d, i, i, i, i, i, i, i, i, d, i, dp, ctypes.c_long, i, d, d]
+        L.orc_cfg_slots.restype = i
+        L.orc_cfg_slots.argtypes = [vp]
+        L.orc_env_get_profiles.argtypes = [vp, dp, dp]
         L.orc_cfg_free.argtypes = [vp]
         L.orc_cfg_tables.restype = i
         L.orc_cfg_tables.argtypes = [vp, dp, dp, dp, dp, dp]
@@ -106,7 +109,8 @@ class OracleConfig:
                  battery_system_available_in_model=True, vehicle_to_everything=False,
                  enable_different_vehicle_battery_capacities=True, enable_requested_state_of_charge=False,
                  time_interval="", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse",
-                 numpy_legacy_promotion=False, grid_cost_weight=0.75, **_ignored):
+                 numpy_legacy_promotion=False, grid_cost_weight=0.75, extended_day=False, pv_noise=0.0,
+                 price_noise=0.0, **_ignored):
         self.N = int(number_of_chargers)
         self.dt = parse_time_interval(time_interval)
         self.T = int(24 / self.dt)
@@ -120,22 +124,24 @@ class OracleConfig:
             int(bool(enable_different_vehicle_battery_capacities)), int(bool(enable_requested_state_of_charge)),
             PENALTY_MODES.get(vehicle_uncharged_penalty_mode, 4), int(charging_mode == "bounded"),
             int(bool(numpy_legacy_promotion)), float(grid_cost_weight), int(price_model),
-            _ptr(irr, ctypes.c_double), irr.size)
+            _ptr(irr, ctypes.c_double), irr.size, int(bool(extended_day)), float(pv_noise), float(price_noise))
         if not self.ptr:
             raise ValueError("oracle: unsupported configuration")
         self.obs_dim = (1 + self.pv) * 4 + 2 * self.N + int(self.bess)
         self.act_dim = self.N + int(self.bess)
+        self.slots = lib().orc_cfg_slots(self.ptr)   # 25 (charger.py:16-19), T+1 for the extended day
+        self.n_price = 2 * self.T if extended_day else 48
 
     def tables(self):
         irr = np.zeros(512)
         pv = np.zeros(512)
-        price = np.zeros(48)
+        price = np.zeros(512)
         mx = np.zeros(1)
         pmx = np.zeros(1)
         n = lib().orc_cfg_tables(self.ptr, _ptr(irr, ctypes.c_double), _ptr(mx, ctypes.c_double),
                                  _ptr(pv, ctypes.c_double), _ptr(price, ctypes.c_double),
                                  _ptr(pmx, ctypes.c_double))
-        return dict(irr=irr[:n], irr_max=mx[0], pv_power=pv[:n], price=price, price_max=pmx[0])
+        return dict(irr=irr[:n], irr_max=mx[0], pv_power=pv[:n], price=price[:self.n_price], price_max=pmx[0])
 
     def __del__(self):
         if getattr(self, "ptr", None) and _lib is not None:
@@ -148,6 +154,9 @@ class OracleEnv:
     def __init__(self, cfg, seed=0):
         self.cfg = cfg
         self.ptr = lib().orc_env_new(cfg.ptr, int(seed))
+        if not self.ptr:
+            raise IndexError("oracle: this time interval needs extended_day=True "
+                             "(the reference's 25-slot arrays, charger.py:16-19)")
 
     def __del__(self):
         if getattr(self, "ptr", None) and _lib is not None:
@@ -176,7 +185,8 @@ class OracleEnv:
 
     def load(self, soc, occ, cap, req, arrivals, departures, ratio):
         N = self.cfg.N
-        f = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).reshape(N, SLOTS))
+        S = self.cfg.slots
+        f = lambda a: np.ascontiguousarray(np.asarray(a, np.float64).reshape(N, S))
         soc, occ, cap, req = f(soc), f(occ), f(cap), f(req)
         arr = np.ascontiguousarray(np.asarray(arrivals, np.int32).reshape(N, -1))
         dep = np.ascontiguousarray(np.asarray(departures, np.int32).reshape(N, -1))
@@ -201,13 +211,20 @@ class OracleEnv:
 
     def scenario(self, vmax=8):
         N = self.cfg.N
-        soc, occ, cap, req = (np.zeros((N, SLOTS)) for _ in range(4))
+        soc, occ, cap, req = (np.zeros((N, self.cfg.slots)) for _ in range(4))
         arr = np.zeros((N, vmax), np.int32)
         dep = np.zeros((N, vmax), np.int32)
         lib().orc_env_get_scenario(self.ptr, _ptr(soc, ctypes.c_double), _ptr(occ, ctypes.c_double),
                                    _ptr(cap, ctypes.c_double), _ptr(req, ctypes.c_double),
                                    _ptr(arr, ctypes.c_int), _ptr(dep, ctypes.c_int), vmax)
         return dict(soc=soc, occ=occ, cap=cap, req=req, arrivals=arr, departures=dep)
+
+    def profiles(self):
+        """This day's PV / price profile factors [T + 3] (build-defined stochastic profiles)."""
+        n = self.cfg.T + 3
+        fpv, fpr = np.zeros(n), np.zeros(n)
+        lib().orc_env_get_profiles(self.ptr, _ptr(fpv, ctypes.c_double), _ptr(fpr, ctypes.c_double))
+        return fpv, fpr
 
 
 class OracleRng:

@@ -24,7 +24,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define ORC_SLOTS 25      /* charger.py:16-19 fixed 25-slot arrays */
 #define ORC_MAXV 32       /* max vehicles per charger per day (list capacity) */
 #define ORC_MAXT 128
 #define MT_N 624
@@ -133,6 +132,55 @@ int64_t orc_py_randint(orc_mt *s, int64_t a, int64_t b) {
 }
 
 /* ------------------------------------------------------------------------------
+ * Build-defined generalisation, off by default:
+ *
+ *   extended_day   days longer than 24 steps (dt < 1 h).  The reference cannot run them
+ *                  (25-slot arrays, charger.py:16-19; 48-entry price table, accountant.py:49).
+ *                  Here the per-charger arrays get T+1 slots (python index -1 -> slot T), the
+ *                  price table gets 2T entries from the per-step tariff loop the reference
+ *                  computes but does not use (accountant.py:61-68; models 1-4: the hourly
+ *                  value of hour floor(i*dt)), the PV table is the dt-window mean as for any
+ *                  dt (pv_system_manager.py:34-44), the generator is the reference's own
+ *                  dt-scaled one, and the departure observation keeps its literal /24.
+ *   pv_noise,      stochastic PV and price profiles: per env and day, every table entry k used
+ *   price_noise    (reward at t, observation t..t+3) is scaled by f = 1 + sigma * z(k), z in
+ *                  [-1, 1) from a counter-based hash of (env seed, day, domain, k).  sigma = 0
+ *                  gives f = 1 exactly.
+ *
+ * There is no reference oracle for these: parity is against this restatement only.
+ * ---------------------------------------------------------------------------- */
+#define ORC_REF_SLOTS 25
+#define ORC_MAXN 256
+#define ORC_MAXSLOTS (ORC_MAXT + 1)
+
+/* triple32 integer hash and the stream key shared with the GPU generator
+ * (smart-nanogrid-gym_amd/csrc/sng_kernels.hip: mix32, stream_key). */
+static uint32_t mix32(uint32_t x) {
+    x ^= x >> 17; x *= 0xed5ad4bbu;
+    x ^= x >> 11; x *= 0xac4c1b51u;
+    x ^= x >> 15; x *= 0x31848babu;
+    x ^= x >> 14;
+    return x;
+}
+
+static uint32_t stream_key(uint64_t seed, uint64_t ge, uint32_t lane, uint64_t day) {
+    uint32_t k0 = mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + (uint32_t)day * 0x9e3779b9u));
+    uint32_t k1 = mix32(k0 ^ (uint32_t)ge);
+    return mix32(k1 ^ ((uint32_t)(ge >> 32) * 0x85ebca6bu + lane * 0xc2b2ae35u + 0x27d4eb2fu));
+}
+
+#define ORC_DOMAIN_PV 0x50560000u
+#define ORC_DOMAIN_PRICE 0x50520000u
+
+/* profile factor 1 + sigma * z, z = h * 2^-31 - 1 in [-1, 1) */
+static double profile_factor(uint64_t env_seed, uint32_t domain, uint64_t day, int k, double sigma) {
+    uint32_t key = stream_key(env_seed, 0, domain, day);
+    uint32_t h = mix32(key + (uint32_t)k * 0x9e3779b9u);
+    double z = (double)h * 0x1.0p-31 - 1.0;
+    return 1.0 + sigma * z;
+}
+
+/* ------------------------------------------------------------------------------
  * Configuration and constant tables
  * ---------------------------------------------------------------------------- */
 enum { PEN_NONE = 0, PEN_ON_DEPARTURE = 1, PEN_SPARSE = 2, PEN_DENSE = 3, PEN_INVALID = 4 };
@@ -148,12 +196,16 @@ typedef struct {
     int bounded;             /* charging_mode == 'bounded' */
     int numpy_legacy;        /* 1: NumPy<2 promotion (action*22*0.95 in f64) */
     double grid_cost_weight; /* accountant.py:222 (0.75 in v1; 0.8 in the recorded KATs) */
+    int extended;            /* build-defined extended day (see above) */
+    int slots;               /* per-charger array length: 25 (charger.py:16-19), T+1 when extended */
+    double pv_noise, price_noise;
     /* tables, built by orc_build_tables */
     int n_irr;
     double irr[4 * ORC_MAXT];       /* solar_irradiance_2[0, :], pv_system_manager.py:322-353 */
     double irr_max;
     double pv_power[4 * ORC_MAXT];  /* available_solar_power[0, :], :355-376 */
-    double price[48];               /* energy_price[0, :], accountant.py:235-288 */
+    int n_price;
+    double price[4 * ORC_MAXT];     /* energy_price[0, :], accountant.py:235-288 (48 entries) */
     double price_max;
 } orc_cfg;
 
@@ -221,9 +273,22 @@ int orc_build_tables(orc_cfg *c, int price_model, const double *irr_min, long n_
         case 4: memcpy(day, m4, sizeof day); break;
         default: return -1;   /* model 5 raises TypeError (:277-278), others a shape error */
     }
-    for (int k = 0; k < 48; k++) c->price[k] = day[k % 24];   /* concatenate twice, :287 */
+    if (!c->extended) {
+        c->n_price = 48;
+        for (int k = 0; k < 48; k++) c->price[k] = day[k % 24];   /* concatenate twice, :287 */
+    } else {
+        /* per-step tariffs: the loop of accountant.py:61-68 for model 0, the hourly value otherwise */
+        c->n_price = 2 * T;
+        for (int i = 0; i < T; i++) {
+            double v;
+            if (price_model == 0) v = (i < 7 / c->dt || i > 19 / c->dt) ? low : high;
+            else v = day[(int)floor(i * c->dt) % 24];
+            c->price[i] = v;
+            c->price[i + T] = v;
+        }
+    }
     mx = 0.0;
-    for (int k = 0; k < 48; k++) if (c->price[k] >= 0 && c->price[k] > mx) mx = c->price[k];
+    for (int k = 0; k < c->n_price; k++) if (c->price[k] >= 0 && c->price[k] > mx) mx = c->price[k];
     c->price_max = mx;                                   /* :238 */
     return 0;
 }
@@ -232,21 +297,25 @@ int orc_build_tables(orc_cfg *c, int price_model, const double *irr_min, long n_
  * One environment, in the reference's own data structures
  * ---------------------------------------------------------------------------- */
 typedef struct {
-    double soc[ORC_SLOTS], cap[ORC_SLOTS], occ[ORC_SLOTS], req[ORC_SLOTS];  /* charger.py:16-19 */
-    int arrivals[ORC_MAXV], n_arr;                                          /* charger.vehicle_arrivals */
-    int departures[ORC_MAXV], n_dep;                                        /* ChargingStation.departures[c] */
-    double nonexistent;                                                     /* charger.py:146-156 */
+    double *soc, *cap, *occ, *req;              /* charger.py:16-19, cfg->slots entries each */
+    int arrivals[ORC_MAXV], n_arr;              /* charger.vehicle_arrivals */
+    int departures[ORC_MAXV], n_dep;            /* ChargingStation.departures[c] */
+    double nonexistent;                         /* charger.py:146-156 */
 } orc_charger;
 
 typedef struct {
     const orc_cfg *cfg;
     orc_mt np_rng, py_rng;          /* global numpy / python RNG streams */
+    uint64_t seed;                  /* this env's seed (profile noise key) */
+    uint64_t day;                   /* resets so far (profile noise key) */
     int t;
     double ratio;                   /* random_pv_shift_ratio */
     double bess_soc, bess_init;     /* battery_energy_storage_system.py:166-178, initial 0.5 */
     double bess_power, bess_calc_power;
-    int penalty_list[256], n_penalty;  /* ChargingStation._penalty_check_vehicles */
-    orc_charger ch[256];
+    int penalty_list[ORC_MAXN], n_penalty;  /* ChargingStation._penalty_check_vehicles */
+    double f_pv[ORC_MAXT + 4], f_price[ORC_MAXT + 4];   /* this day's profile factors */
+    orc_charger *ch;
+    double *slotbuf;
 } orc_env;
 
 /* Step record (the 28-key results dict subset the parity tests compare). */
@@ -257,23 +326,58 @@ typedef struct {
                                       2 = ValueError charging mode, 3 = ValueError BESS SoC > 1 */
 } orc_step_out;
 
-static int slot_index(int t) { return t < 0 ? ORC_SLOTS + t : t; }   /* python negative index */
+static int slot_index(const orc_cfg *c, int t) { return t < 0 ? c->slots + t : t; }   /* python negative index */
 
 static int in_list(const int *l, int n, int v) {
     for (int i = 0; i < n; i++) if (l[i] == v) return 1;
     return 0;
 }
 
-size_t orc_env_size(void) { return sizeof(orc_env); }
+static void charger_clear(orc_env *e, orc_charger *ch) {
+    int S = e->cfg->slots;
+    memset(ch->soc, 0, sizeof(double) * S); memset(ch->cap, 0, sizeof(double) * S);
+    memset(ch->occ, 0, sizeof(double) * S); memset(ch->req, 0, sizeof(double) * S);
+    ch->n_arr = ch->n_dep = 0;
+    ch->nonexistent = 0.0;
+}
 
-void orc_env_init(orc_env *e, const orc_cfg *cfg, uint64_t seed) {
-    memset(e, 0, sizeof *e);
-    e->cfg = cfg;
+orc_env *orc_env_new(const orc_cfg *c, uint64_t seed) {
+    if (!c->extended && c->T > ORC_REF_SLOTS - 1) return NULL;   /* IndexError in the reference */
+    orc_env *e = (orc_env *)calloc(1, sizeof(orc_env));
+    if (!e) return NULL;
+    e->cfg = c;
+    e->ch = (orc_charger *)calloc((size_t)c->n_chargers, sizeof(orc_charger));
+    e->slotbuf = (double *)calloc((size_t)c->n_chargers * 4 * c->slots, sizeof(double));
+    if (!e->ch || !e->slotbuf) { free(e->ch); free(e->slotbuf); free(e); return NULL; }
+    for (int i = 0; i < c->n_chargers; i++) {
+        double *b = e->slotbuf + (size_t)i * 4 * c->slots;
+        e->ch[i].soc = b; e->ch[i].cap = b + c->slots; e->ch[i].occ = b + 2 * c->slots; e->ch[i].req = b + 3 * c->slots;
+    }
     orc_np_seed(&e->np_rng, (uint32_t)seed);
     orc_py_seed(&e->py_rng, seed);
+    e->seed = seed;
+    e->day = 0;
     e->bess_soc = 0.5;     /* central_management_system.py:35 */
     e->bess_init = 0.5;
     e->ratio = 1.0;        /* smart_nanogrid_environment.py:74 */
+    return e;
+}
+
+void orc_env_free(orc_env *e) {
+    if (!e) return;
+    free(e->ch);
+    free(e->slotbuf);
+    free(e);
+}
+
+/* The day's profile factors (build-defined; all 1.0 when both sigmas are 0). */
+static void draw_profiles(orc_env *e) {
+    const orc_cfg *c = e->cfg;
+    for (int k = 0; k < c->T + 3; k++) {
+        e->f_pv[k] = c->pv_noise != 0.0 ? profile_factor(e->seed, ORC_DOMAIN_PV, e->day, k, c->pv_noise) : 1.0;
+        e->f_price[k] = c->price_noise != 0.0 ? profile_factor(e->seed, ORC_DOMAIN_PRICE, e->day, k, c->price_noise) : 1.0;
+    }
+    e->day += 1;
 }
 
 /* ChargingStation.generate_random_vehicle_departure_time, charging_station.py:271-279 */
@@ -360,10 +464,13 @@ static int observe(orc_env *e, float *obs) {
     const orc_cfg *c = e->cfg;
     int t = e->t, N = c->n_chargers, k = 0;
     penalty_check(e, t);
-    if (c->pv) obs[k++] = (float)((c->irr[t] / c->irr_max) * e->ratio);
-    obs[k++] = (float)(c->price[t] / c->price_max);
-    if (c->pv) for (int j = t + 1; j < t + 4 && j < c->n_irr; j++) obs[k++] = (float)((c->irr[j] / c->irr_max) * e->ratio);
-    for (int j = t + 1; j < t + 4 && j < 48; j++) obs[k++] = (float)(c->price[j] / c->price_max);
+    if (c->pv) obs[k++] = (float)(((c->irr[t] / c->irr_max) * e->ratio) * e->f_pv[t]);
+    obs[k++] = (float)((c->price[t] / c->price_max) * e->f_price[t]);
+    if (c->pv)
+        for (int j = t + 1; j < t + 4 && j < c->n_irr; j++)
+            obs[k++] = (float)(((c->irr[j] / c->irr_max) * e->ratio) * e->f_pv[j]);
+    for (int j = t + 1; j < t + 4 && j < c->n_price; j++)
+        obs[k++] = (float)((c->price[j] / c->price_max) * e->f_price[j]);
     for (int i = 0; i < N; i++) obs[k++] = (float)e->ch[i].soc[t];   /* extract_current_state_of_charge, :114-117 */
     for (int i = 0; i < N; i++) {                                      /* calculate_departure_times, :92-112 */
         orc_charger *ch = &e->ch[i];
@@ -384,24 +491,26 @@ int orc_env_reset(orc_env *e, float *obs) {
     const orc_cfg *c = e->cfg;
     e->t = 0;
     for (int i = 0; i < c->n_chargers; i++) {
-        memset(&e->ch[i], 0, sizeof(orc_charger));
+        charger_clear(e, &e->ch[i]);
         gen_charger(e, &e->ch[i]);
     }
     e->ratio = (double)orc_py_randint(&e->py_rng, 0, 180) / 100;   /* :358 */
+    draw_profiles(e);
     return observe(e, obs);
 }
 
-/* Injected scenario (for known-answer replays): per-charger 25-slot arrays + lists. */
+/* Injected scenario (for known-answer replays): per-charger slot arrays + lists. */
 int orc_env_load(orc_env *e, const double *soc, const double *occ, const double *cap, const double *req,
                  const int *arrivals, const int *departures, int vmax, double ratio, float *obs) {
     const orc_cfg *c = e->cfg;
+    int S = c->slots;
     e->t = 0;
     for (int i = 0; i < c->n_chargers; i++) {
         orc_charger *ch = &e->ch[i];
-        memset(ch, 0, sizeof *ch);
-        for (int s = 0; s < ORC_SLOTS; s++) {
-            ch->soc[s] = soc[i * ORC_SLOTS + s]; ch->occ[s] = occ[i * ORC_SLOTS + s];
-            ch->cap[s] = cap[i * ORC_SLOTS + s]; ch->req[s] = req[i * ORC_SLOTS + s];
+        charger_clear(e, ch);
+        for (int s = 0; s < S; s++) {
+            ch->soc[s] = soc[i * S + s]; ch->occ[s] = occ[i * S + s];
+            ch->cap[s] = cap[i * S + s]; ch->req[s] = req[i * S + s];
         }
         for (int v = 0; v < vmax; v++) {
             if (arrivals[i * vmax + v] >= 0) ch->arrivals[ch->n_arr++] = arrivals[i * vmax + v];
@@ -409,6 +518,7 @@ int orc_env_load(orc_env *e, const double *soc, const double *occ, const double 
         }
     }
     e->ratio = ratio;
+    draw_profiles(e);
     return observe(e, obs);
 }
 
@@ -423,7 +533,7 @@ static double charger_step(orc_env *e, orc_charger *ch, float a, int t, int *err
     const orc_cfg *c = e->cfg;
     double dt = c->dt;
     int arrived = in_list(ch->arrivals, ch->n_arr, t);
-    int prev = arrived ? t : slot_index(t - 1);
+    int prev = arrived ? t : slot_index(c, t - 1);
     double power;
     if (a == 0) {
         power = 0.0;
@@ -485,7 +595,7 @@ int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out
     if (t == 0 && c->bess) e->bess_init = e->bess_soc;                 /* :93-94 */
 
     /* simulate_vehicle_charging, charging_station.py:281-300 */
-    double power[256], pos[256] = {0}, neg[256] = {0};
+    double power[ORC_MAXN], pos[ORC_MAXN] = {0}, neg[ORC_MAXN] = {0};
     int npos = 0, nneg = 0, err = 0;
     for (int i = 0; i < N; i++) {
         orc_charger *ch = &e->ch[i];
@@ -511,11 +621,11 @@ int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out
     double pen_v = 0;
     for (int k = 0; k < e->n_penalty; k++) {
         orc_charger *ch = &e->ch[e->penalty_list[k]];
-        int s = slot_index(t - 1);
+        int s = slot_index(c, t - 1);
         pen_v += vehicle_penalty(ch->req[s], ch->soc[s]);
     }
 
-    double solar = c->pv ? c->pv_power[t] * e->ratio : 0;              /* :99-103 */
+    double solar = c->pv ? (c->pv_power[t] * e->ratio) * e->f_pv[t] : 0;   /* :99-103 */
     double demand = p_ch + p_dis;                                       /* :105 */
     if (demand < 0 && !c->v2x) err = 1;                                 /* :158-159 */
     else if (demand < 0 && c->v2x) out->breakpoint = 1;                 /* :160-165 */
@@ -550,7 +660,7 @@ int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out
     }
     double grid = rem;
     double energy = grid * c->dt;                                       /* :107 */
-    double price = c->price[t];
+    double price = c->price[t] * e->f_price[t];
     double cost = energy < 0 ? (energy * 0.8) * price : energy * price; /* accountant.py:213-219 */
     double total_pen = 0.8 * pen_b + pen_v;                             /* penaliser.py:177-181 */
     double total = c->grid_cost_weight * fabs(cost) + total_pen;        /* accountant.py:221-223 */
@@ -577,26 +687,25 @@ int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out
 }
 
 /* Batched driver used for the CPU baseline: E independent environments, each stepped
- * through `episodes` full days with actions[ep][t][env][A]; returns the sum of rewards. */
+ * through `episodes` full days with actions[t][env][A]; returns the sum of rewards. */
 double orc_run_batch(const orc_cfg *cfg, int64_t n_envs, uint64_t seed, int episodes,
                      const float *actions, int64_t act_stride_env, float *obs_scratch) {
-    orc_env *e = (orc_env *)malloc(sizeof(orc_env));
     double acc = 0;
     orc_step_out out;
-    int T = cfg->T, A = cfg->n_chargers + (cfg->bess ? 1 : 0);
+    int T = cfg->T;
     for (int64_t i = 0; i < n_envs; i++) {
-        orc_env_init(e, cfg, seed + (uint64_t)i);
+        orc_env *e = orc_env_new(cfg, seed + (uint64_t)i);
+        if (!e) return NAN;
         for (int ep = 0; ep < episodes; ep++) {
             orc_env_reset(e, obs_scratch);
             for (int t = 0; t < T; t++) {
                 const float *a = actions + ((int64_t)t * n_envs + i) * act_stride_env;
-                (void)A;
                 orc_env_step(e, a, obs_scratch, &out);
                 acc += out.reward;
             }
         }
+        orc_env_free(e);
     }
-    free(e);
     return acc;
 }
 
@@ -605,13 +714,18 @@ double orc_run_batch(const orc_cfg *cfg, int64_t n_envs, uint64_t seed, int epis
  * ---------------------------------------------------------------------------- */
 orc_cfg *orc_cfg_new(int n_chargers, double dt, int pv, int bess, int v2x, int diff_caps, int req_enabled,
                      int penalty_mode, int bounded, int numpy_legacy, double grid_cost_weight, int price_model,
-                     const double *irr_min, long n_min) {
-    if (n_chargers < 1 || n_chargers > 256) return NULL;
+                     const double *irr_min, long n_min, int extended, double pv_noise, double price_noise) {
+    if (n_chargers < 1 || n_chargers > ORC_MAXN) return NULL;
     orc_cfg *c = (orc_cfg *)calloc(1, sizeof(orc_cfg));
     c->n_chargers = n_chargers;
     c->dt = dt;
     c->T = (int)(24 / dt);
+    c->extended = extended;
+    /* a standard config with T > 24 only builds tables (the reference's own tables exist for any dt,
+     * its 25-slot arrays do not run); orc_env_new refuses it */
     if (c->T < 1 || c->T > ORC_MAXT) { free(c); return NULL; }
+    c->slots = extended ? c->T + 1 : ORC_REF_SLOTS;
+    c->pv_noise = pv_noise; c->price_noise = price_noise;
     c->pv = pv; c->bess = bess; c->v2x = v2x; c->diff_caps = diff_caps; c->req_enabled = req_enabled;
     c->penalty_mode = penalty_mode; c->bounded = bounded; c->numpy_legacy = numpy_legacy;
     c->grid_cost_weight = grid_cost_weight;
@@ -621,23 +735,17 @@ orc_cfg *orc_cfg_new(int n_chargers, double dt, int pv, int bess, int v2x, int d
 
 void orc_cfg_free(orc_cfg *c) { free(c); }
 
+int orc_cfg_slots(const orc_cfg *c) { return c->slots; }
+
 int orc_cfg_tables(const orc_cfg *c, double *irr, double *irr_max, double *pv_power, double *price,
                    double *price_max) {
     memcpy(irr, c->irr, sizeof(double) * c->n_irr);
     memcpy(pv_power, c->pv_power, sizeof(double) * c->n_irr);
-    memcpy(price, c->price, sizeof(double) * 48);
+    memcpy(price, c->price, sizeof(double) * c->n_price);
     *irr_max = c->irr_max;
     *price_max = c->price_max;
     return c->n_irr;
 }
-
-orc_env *orc_env_new(const orc_cfg *c, uint64_t seed) {
-    orc_env *e = (orc_env *)malloc(sizeof(orc_env));
-    orc_env_init(e, c, seed);
-    return e;
-}
-
-void orc_env_free(orc_env *e) { free(e); }
 
 int orc_env_t(const orc_env *e) { return e->t; }
 
@@ -655,20 +763,27 @@ int orc_env_step_flat(orc_env *e, const float *actions, float *obs, double *out,
     return err;
 }
 
-/* Export the current scenario in the reference's layout (25-slot arrays, padded lists). */
+/* Export the current scenario in the reference's layout (slot arrays, padded lists). */
 void orc_env_get_scenario(const orc_env *e, double *soc, double *occ, double *cap, double *req,
                           int *arrivals, int *departures, int vmax) {
+    int S = e->cfg->slots;
     for (int i = 0; i < e->cfg->n_chargers; i++) {
         const orc_charger *ch = &e->ch[i];
-        memcpy(soc + i * ORC_SLOTS, ch->soc, sizeof ch->soc);
-        memcpy(occ + i * ORC_SLOTS, ch->occ, sizeof ch->occ);
-        memcpy(cap + i * ORC_SLOTS, ch->cap, sizeof ch->cap);
-        memcpy(req + i * ORC_SLOTS, ch->req, sizeof ch->req);
+        memcpy(soc + i * S, ch->soc, sizeof(double) * S);
+        memcpy(occ + i * S, ch->occ, sizeof(double) * S);
+        memcpy(cap + i * S, ch->cap, sizeof(double) * S);
+        memcpy(req + i * S, ch->req, sizeof(double) * S);
         for (int v = 0; v < vmax; v++) {
             arrivals[i * vmax + v] = v < ch->n_arr ? ch->arrivals[v] : -1;
             departures[i * vmax + v] = v < ch->n_dep ? ch->departures[v] : -1;
         }
     }
+}
+
+/* Profile factors of the current day, [T + 3] each (build-defined noise). */
+void orc_env_get_profiles(const orc_env *e, double *f_pv, double *f_price) {
+    memcpy(f_pv, e->f_pv, sizeof(double) * (e->cfg->T + 3));
+    memcpy(f_price, e->f_price, sizeof(double) * (e->cfg->T + 3));
 }
 
 /* RNG probes for the draw-for-draw tests against numpy / Python's random. */
