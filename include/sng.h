@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 2
+#define SNG_ABI_VERSION 3
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -102,6 +102,15 @@ typedef struct SngConfig {
     int64_t irradiance_minutes;
     /* Kernel tuning: GPU lanes per environment in the step kernel (0 = automatic; 1, 2, 4). */
     int32_t step_lanes_per_env;
+    /* Build-defined generalisation (no reference oracle, default off):
+     * extended_day = 1 allows days longer than 24 steps (dt < 1 h): per-charger arrays get
+     * T+1 slots, prices come from the per-step tariff loop (accountant.py:61-68).
+     * pv_noise / price_noise = sigma > 0 scale every PV / price table entry an env uses on a day
+     * by 1 + sigma*z, z in [-1, 1) from a counter-based hash of (env seed, day, k). */
+    int32_t extended_day;
+    int32_t reserved0;
+    double pv_noise;
+    double price_noise;
 } SngConfig;
 
 typedef struct SngDims {
@@ -111,7 +120,7 @@ typedef struct SngDims {
     int32_t number_of_chargers;
     int64_t num_envs;
     int32_t step_lanes_per_env;   /* lanes per env the step kernel runs with (SngConfig 0 = default) */
-    int32_t reserved;
+    int32_t slots;                /* per-charger scenario array length: 25, or T+1 with extended_day */
 } SngDims;
 
 /* Optional per-step diagnostics: device pointers, each [num_envs]; NULL = not written.
@@ -139,7 +148,7 @@ typedef struct SngInfo {
  * generate_new_initial_values / load_initial_values, charging_station.py:119-186):
  * per env and charger, 25-slot arrays plus padded arrival/departure lists (-1 = none). */
 typedef struct SngScenario {
-    int32_t slots;                 /* 25 (charger.py:16-19) */
+    int32_t slots;                 /* 25 (charger.py:16-19); T+1 with extended_day */
     int32_t max_vehicles;          /* padded list length */
     const double *soc;             /* [num_envs][N][slots]  'SOC' */
     const double *occupancy;       /* [num_envs][N][slots]  'Charger_occupancy' */

@@ -26,6 +26,7 @@ hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, do
                            int vec_io, hipStream_t stream);
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            hipStream_t stream);
+hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream);
 int step_lanes_supported(int n, int lanes);
 }  // namespace sng
 
@@ -108,8 +109,20 @@ bool build_tables(const SngConfig &c, int T, HostTables &tb, std::string &err) {
             err = "price_model must be 0..4 (model 5 raises TypeError in accountant.py:277-278)";
             return false;
     }
-    tb.price.assign(kPriceLen, 0.0);
-    for (int k = 0; k < kPriceLen; ++k) tb.price[k] = day[k % 24];   // concatenate([day, day]), :287
+    if (!c.extended_day) {
+        tb.price.assign(kPriceLen, 0.0);
+        for (int k = 0; k < kPriceLen; ++k) tb.price[k] = day[k % 24];   // concatenate([day, day]), :287
+    } else {
+        // build-defined extended day: the per-step tariff loop of accountant.py:61-68 for model 0,
+        // the hourly value of hour floor(i*dt) for models 1-4; concatenated twice
+        tb.price.assign(2 * T, 0.0);
+        for (int i = 0; i < T; ++i) {
+            const double v = (c.price_model == 0) ? ((i < 7 / dt || i > 19 / dt) ? low : high)
+                                                  : day[(int)std::floor(i * dt) % 24];
+            tb.price[i] = v;
+            tb.price[i + T] = v;
+        }
+    }
     mx = 0.0;
     for (double v : tb.price)
         if (v >= 0 && v > mx) mx = v;
@@ -131,9 +144,10 @@ int list_len(const int32_t *l, int V) {
 
 // One day of one environment in the reference's layout.
 struct DayView {
-    double *soc, *occ, *cap, *req;   // [N][25]
+    double *soc, *occ, *cap, *req;   // [N][S]
     int32_t *arr, *dep;              // [N][V], -1 padded
     int V;
+    int S;                           // slots per charger: 25 (charger.py:16-19), T+1 with extended_day
 };
 
 // ChargingStation.generate_initial_vehicle_presence_per_charger and the draws it makes
@@ -141,15 +155,15 @@ struct DayView {
 bool generate_day(const SngConfig &c, int T, MT19937 &rng, DayView d) {
     const int N = c.number_of_chargers;
     const double dt = c.time_interval_hours;
-    std::fill(d.soc, d.soc + N * kSlots, 0.0);
-    std::fill(d.occ, d.occ + N * kSlots, 0.0);
-    std::fill(d.cap, d.cap + N * kSlots, 0.0);
-    std::fill(d.req, d.req + N * kSlots, 0.0);
+    const int S = d.S;
+    std::fill(d.soc, d.soc + N * S, 0.0);
+    std::fill(d.occ, d.occ + N * S, 0.0);
+    std::fill(d.cap, d.cap + N * S, 0.0);
+    std::fill(d.req, d.req + N * S, 0.0);
     std::fill(d.arr, d.arr + N * d.V, -1);
     std::fill(d.dep, d.dep + N * d.V, -1);
     for (int ch = 0; ch < N; ++ch) {
-        double *soc = d.soc + ch * kSlots, *occ = d.occ + ch * kSlots, *cap = d.cap + ch * kSlots,
-               *req = d.req + ch * kSlots;
+        double *soc = d.soc + ch * S, *occ = d.occ + ch * S, *cap = d.cap + ch * S, *req = d.req + ch * S;
         int32_t *arr = d.arr + ch * d.V, *dep_l = d.dep + ch * d.V;
         int na = 0;
         bool present = false, cap_gen = false, req_gen = false;
@@ -230,8 +244,8 @@ bool encode_day(const Params &p, int64_t E, int64_t e, const DayView &d, uint32_
     const int N = p.n, T = p.T;
     double pen_t0 = 0.0;
     for (int c = 0; c < N; ++c) {
-        const double *soc = d.soc + c * kSlots, *occ = d.occ + c * kSlots, *cap = d.cap + c * kSlots,
-                     *req = d.req + c * kSlots;
+        const int S = d.S;
+        const double *soc = d.soc + c * S, *occ = d.occ + c * S, *cap = d.cap + c * S, *req = d.req + c * S;
         const int32_t *arr = d.arr + c * d.V, *dep = d.dep + c * d.V;
         const int na = list_len(arr, d.V), nd = list_len(dep, d.V);
         for (int t = 0; t < T; ++t) {
@@ -242,7 +256,7 @@ bool encode_day(const Params &p, int64_t E, int64_t e, const DayView &d, uint32_
             }
             const bool occupied = (o == 1.0);
             const bool arrived = in_list(arr, na, t);
-            const int prev = arrived ? t : (t >= 1 ? t - 1 : kSlots - 1);   // python index t-1
+            const int prev = arrived ? t : (t >= 1 ? t - 1 : S - 1);   // python index t-1
             // SOC[prev] is the running value only when step t-1 wrote it (charger occupied at t-1)
             const bool running = !arrived && t >= 1 && occ[t - 1] == 1.0;
             uint32_t capv = 0, rem = 0;
@@ -288,7 +302,7 @@ bool encode_day(const Params &p, int64_t E, int64_t e, const DayView &d, uint32_
         }
         // penalty at t = 0 reads python index -1 (slot 24) of SOC / Requested_SOC (penaliser.py:59-69)
         if (occ[0] != 0.0 && penalty_window(p.penalty_mode, dep, nd, 0)) {
-            const double rq = req[kSlots - 1], cur = soc[kSlots - 1];
+            const double rq = req[S - 1], cur = soc[S - 1];
             if (cur < rq - 0.05 * rq) {
                 const double x = (rq - cur) * 10;
                 pen_t0 += x * x;
@@ -330,6 +344,7 @@ struct SngEnv {
     int t = -1;                       // -1: never reset; T: day finished
     bool day_finished = false;
     int i4 = 0, i10 = 0, i1 = 0;
+    int slots = kSlots;               // per-charger array length of scenarios (T+1 with extended_day)
     DeviceState ds{};
     Tables *d_tables = nullptr;
     // host staging (pinned) for days built on the CPU
@@ -423,6 +438,7 @@ int upload_and_observe(SngEnv *env, bool need_req, float *obs, hipStream_t st) {
     HIP_TRY(env, hipMemcpyAsync(env->ds.pen0, env->h_pen0, env->E * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipEventRecord(env->staging_done, st));
     env->p.req_stream = need_req ? 1 : 0;
+    HIP_TRY(env, sng::launch_profiles(env->p, env->ds, env->E, st));
     HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st));
     env->t = 0;
     env->day_finished = false;
@@ -480,9 +496,15 @@ static int validate(const SngConfig *c, int *T_out, std::string &err) {
         err = "24h / time_interval must be an integer (the reference never ends the day otherwise)";
         return SNG_ERR_UNSUPPORTED;
     }
-    if (T > 24) {
-        err = "time intervals below 1h are not runnable in the reference (25-slot arrays, charger.py:16-19)";
+    if (T > 24 && !c->extended_day) {
+        err = "time intervals below 1h are not runnable in the reference (25-slot arrays, charger.py:16-19); "
+              "set extended_day for the build-defined extension";
         return SNG_ERR_UNSUPPORTED;
+    }
+    if (T > kMaxT) { err = "at most 128 steps per day"; return SNG_ERR_UNSUPPORTED; }
+    if (!(c->pv_noise >= 0.0 && c->pv_noise <= 1.0) || !(c->price_noise >= 0.0 && c->price_noise <= 1.0)) {
+        err = "pv_noise / price_noise must be in [0, 1]";
+        return SNG_ERR_INVALID_ARGUMENT;
     }
     if (T < 4) { err = "time interval too long (fewer than 4 steps per day)"; return SNG_ERR_UNSUPPORTED; }
     if (c->penalty_mode < 0 || c->penalty_mode > 3) {
@@ -565,6 +587,11 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
     env->i4 = (int)(4 / p.dt);
     env->i10 = (int)(10 / p.dt);
     env->i1 = (int)(1 / p.dt);
+    env->slots = c.extended_day ? T + 1 : kSlots;
+    p.noise = (c.pv_noise > 0.0 || c.price_noise > 0.0) ? 1 : 0;
+    p.pv_noise = c.pv_noise;
+    p.price_noise = c.price_noise;
+    p.seed = seed;
 
     // host copy of the device tables
     Tables ht;
@@ -575,7 +602,7 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
         ht.irr_norm[k] = env->tables.irr[k] / env->tables.irr_max;   // pv_system_manager.py:369-373
         ht.pv_power[k] = env->tables.pv_power[k];
     }
-    for (int k = 0; k < kPriceLen; ++k) {
+    for (int k = 0; k < (int)env->tables.price.size(); ++k) {
         ht.price[k] = env->tables.price[k];
         ht.price_norm[k] = env->tables.price[k] / env->tables.price_max;   // accountant.py:229-233
     }
@@ -603,6 +630,7 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
               alloc((void **)&ds.aux, tl * sizeof(double)) && alloc((void **)&ds.flags, E * sizeof(uint32_t)) &&
               alloc((void **)&ds.episode, sizeof(uint64_t)) && alloc((void **)&env->d_tables, sizeof(Tables));
     if (ok && p.req_enabled) ok = alloc((void **)&ds.req, tl * sizeof(double));
+    if (ok && p.noise) ok = alloc((void **)&ds.prof, 2 * (size_t)(T + 3) * E * sizeof(double));
     if (!ok) {
         std::string msg = g_create_error;
         sng_destroy(env);
@@ -633,8 +661,8 @@ void sng_destroy(SngEnv *env) {
     if (!env) return;
     (void)hipSetDevice(env->device);
     DeviceState &ds = env->ds;
-    void *dev[] = {ds.soc, ds.bess, ds.bess0, ds.ratio, ds.pen0, ds.word, ds.aux, ds.req, ds.flags, ds.episode,
-                   env->d_tables};
+    void *dev[] = {ds.soc, ds.bess, ds.bess0, ds.ratio, ds.pen0, ds.word, ds.aux, ds.req, ds.flags, ds.prof,
+                   ds.episode, env->d_tables};
     for (void *x : dev)
         if (x) (void)hipFree(x);
     void *host[] = {env->h_word, env->h_aux, env->h_req, env->h_ratio, env->h_pen0};
@@ -652,7 +680,7 @@ int sng_get_dims(const SngEnv *env, SngDims *out) {
     out->number_of_chargers = env->p.n;
     out->num_envs = env->E;
     out->step_lanes_per_env = env->p.lanes;
-    out->reserved = 0;
+    out->slots = env->slots;
     return SNG_OK;
 }
 
@@ -679,6 +707,7 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
             if (rc) return rc;
         }
         HIP_TRY(env, launch_generate(env->p, env->ds, env->seed, env->E, env->i4, env->i10, env->i1, st));
+        HIP_TRY(env, launch_profiles(env->p, env->ds, env->E, st));
         HIP_TRY(env, launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st));
         env->t = 0;
         env->day_finished = false;
@@ -704,10 +733,10 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     std::vector<std::string> errs(16);
     std::vector<char> bad(16, 0);
     parallel_for(env->E, [&](int64_t b, int64_t en, int k) {
-        const int V = kMaxVehicles;
-        std::vector<double> soc(N * kSlots), occ(N * kSlots), cap(N * kSlots), req(N * kSlots);
+        const int V = kMaxVehicles, S = env->slots;
+        std::vector<double> soc(N * S), occ(N * S), cap(N * S), req(N * S);
         std::vector<int32_t> arr(N * V), dep(N * V);
-        DayView d{soc.data(), occ.data(), cap.data(), req.data(), arr.data(), dep.data(), V};
+        DayView d{soc.data(), occ.data(), cap.data(), req.data(), arr.data(), dep.data(), V, S};
         bool need = false;
         for (int64_t i = b; i < en; ++i) {
             // the day-end draw of the previous step (smart_nanogrid_environment.py:190)
@@ -734,7 +763,9 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
 
 int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void *stream) {
     if (!env || !sc || !obs) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
-    if (sc->slots != kSlots) return fail(env, SNG_ERR_INVALID_ARGUMENT, "scenario slots must be 25");
+    if (sc->slots != env->slots)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT,
+                    "scenario slots must be " + std::to_string(env->slots) + " (25; T+1 with extended_day)");
     if (!sc->soc || !sc->occupancy || !sc->capacity || !sc->requested_soc || !sc->arrivals || !sc->departures ||
         !sc->pv_ratio || sc->max_vehicles < 1)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "incomplete scenario");
@@ -747,10 +778,11 @@ int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void
     parallel_for(env->E, [&](int64_t b, int64_t en, int k) {
         bool nr = false;
         for (int64_t i = b; i < en; ++i) {
-            const size_t o = (size_t)i * N * kSlots, ol = (size_t)i * N * V;
+            const int S = env->slots;
+            const size_t o = (size_t)i * N * S, ol = (size_t)i * N * V;
             DayView d{const_cast<double *>(sc->soc + o), const_cast<double *>(sc->occupancy + o),
                       const_cast<double *>(sc->capacity + o), const_cast<double *>(sc->requested_soc + o),
-                      const_cast<int32_t *>(sc->arrivals + ol), const_cast<int32_t *>(sc->departures + ol), V};
+                      const_cast<int32_t *>(sc->arrivals + ol), const_cast<int32_t *>(sc->departures + ol), V, S};
             std::string e;
             if (!encode_day(env->p, env->E, i, d, env->h_word, env->h_aux, env->h_req, &env->h_pen0[i], &nr, e)) {
                 bad[k] = 1;
@@ -864,6 +896,7 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
     hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
     if (e == hipSuccess && with_reset) {
         e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, cs);
+        if (e == hipSuccess) e = launch_profiles(p, env->ds, E, cs);
         if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, cs);
     }
     for (int t = 0; e == hipSuccess && t < p.T; ++t)
@@ -924,6 +957,7 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
         if (e == hipSuccess) e = hipEventCreate(&x);
     for (int d = 0; e == hipSuccess && d < days; ++d) {
         e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, st);
+        if (e == hipSuccess) e = launch_profiles(p, env->ds, E, st);
         if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, st);
         for (int t = 0; e == hipSuccess && t < T; ++t) {
             hipEvent_t a = ev[2 * ((size_t)d * T + t)], b = ev[2 * ((size_t)d * T + t) + 1];
@@ -950,6 +984,7 @@ int sng_host_generate_scenarios(const SngConfig *cfg, int64_t num_envs, uint64_t
     if (num_envs < 1 || episodes < 1 || max_vehicles < 1)
         return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "bad sizes");
     const int N = cfg->number_of_chargers;
+    const int S = cfg->extended_day ? T + 1 : kSlots;
     bool overflow = false;
     for (int64_t i = 0; i < num_envs; ++i) {
         MT19937 np_rng, py_rng;
@@ -958,9 +993,8 @@ int sng_host_generate_scenarios(const SngConfig *cfg, int64_t num_envs, uint64_t
         for (int ep = 0; ep < episodes; ++ep) {
             if (ep > 0) (void)py_rng.py_randint(0, 180);   // day-end draw, smart_nanogrid_environment.py:190
             const size_t k = (size_t)ep * num_envs + i;
-            DayView d{soc + k * N * kSlots, occupancy + k * N * kSlots, capacity + k * N * kSlots,
-                      requested_soc + k * N * kSlots, arrivals + k * N * max_vehicles,
-                      departures + k * N * max_vehicles, max_vehicles};
+            DayView d{soc + k * N * S, occupancy + k * N * S, capacity + k * N * S, requested_soc + k * N * S,
+                      arrivals + k * N * max_vehicles, departures + k * N * max_vehicles, max_vehicles, S};
             if (!generate_day(*cfg, T, np_rng, d)) overflow = true;
             pv_ratio[k] = (double)py_rng.py_randint(0, 180) / 100;
         }

@@ -232,18 +232,54 @@ __device__ __forceinline__ void copy_out(float *__restrict__ dst, const float *_
 
 // Observation header (smart_nanogrid_environment.py:199-240, central_management_system.py:53-60):
 // [solar(t), price(t), solar(t+1..t+3), price(t+1..t+3)] with PV, [price(t), price(t+1..t+3)] without.
-// irr / pn point at irr_norm[t] / price_norm[t] (the step kernel's LDS copy, or the tables).
+// irr / pn point at irr_norm[t] / price_norm[t] (the step kernel's LDS copy, or the tables);
+// fpv / fpr are the env's profile factors for t..t+3 (1.0 without stochastic profiles).
 __device__ __forceinline__ void write_obs_header(float *o, const Params &p, const double *irr, const double *pn,
-                                                 double ratio) {
+                                                 double ratio, const double *fpv, const double *fpr) {
     int k = 0;
-    if (p.pv) o[k++] = (float)(irr[0] * ratio);
-    o[k++] = (float)pn[0];
+    if (p.pv) o[k++] = (float)((irr[0] * ratio) * fpv[0]);
+    o[k++] = (float)(pn[0] * fpr[0]);
     if (p.pv) {
 #pragma unroll
-        for (int j = 1; j <= 3; ++j) o[k++] = (float)(irr[j] * ratio);
+        for (int j = 1; j <= 3; ++j) o[k++] = (float)((irr[j] * ratio) * fpv[j]);
     }
 #pragma unroll
-    for (int j = 1; j <= 3; ++j) o[k++] = (float)pn[j];
+    for (int j = 1; j <= 3; ++j) o[k++] = (float)(pn[j] * fpr[j]);
+}
+
+// ---------------------------------------------------------------------------------
+// Counter-based 32-bit hash streams (device generator, stochastic profiles).  The oracle
+// restates mix32 / stream_key / profile_factor bit for bit (oracle/sng_oracle.c).
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {   // "triple32" integer hash (bijective)
+    x ^= x >> 17;
+    x *= 0xed5ad4bbu;
+    x ^= x >> 11;
+    x *= 0xac4c1b51u;
+    x ^= x >> 15;
+    x *= 0x31848babu;
+    x ^= x >> 14;
+    return x;
+}
+
+// Stream key of (seed, global env, charger | domain, day).
+__device__ __forceinline__ uint32_t stream_key(uint64_t seed, uint64_t ge, uint32_t lane, uint64_t day) {
+    const uint32_t k0 = mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + (uint32_t)day * 0x9e3779b9u));
+    const uint32_t k1 = mix32(k0 ^ (uint32_t)ge);
+    return mix32(k1 ^ ((uint32_t)(ge >> 32) * 0x85ebca6bu + lane * 0xc2b2ae35u + 0x27d4eb2fu));
+}
+
+constexpr uint32_t kDomainPV = 0x50560000u;
+constexpr uint32_t kDomainPrice = 0x50520000u;
+
+// Build-defined stochastic profile factor 1 + sigma * z, z = h * 2^-31 - 1 in [-1, 1), of table
+// entry k for the env with seed env_seed on day `day` (SngConfig.pv_noise / price_noise).
+__device__ __forceinline__ double profile_factor(uint64_t env_seed, uint32_t domain, uint64_t day, int k,
+                                                 double sigma) {
+    const uint32_t key = stream_key(env_seed, 0, domain, day);
+    const uint32_t h = mix32(key + (uint32_t)k * 0x9e3779b9u);
+    const double z = (double)h * 0x1.0p-31 - 1.0;
+    return 1.0 + sigma * z;
 }
 
 // Per-step constants staged in LDS by the step kernel: irr_norm[t..t+3], price_norm[t..t+3],
@@ -357,10 +393,10 @@ template <bool DIAG>
 __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, const InfoPtrs &info, int64_t e,
                                          int t, double ratio, double bess, float bess_action, double p_ch,
                                          double p_dis, double pen_v, double nonexist, uint32_t fl, float *o_row,
-                                         const double *cst, double ret_prev, double bess0, double *__restrict__ reward,
-                                         uint8_t *__restrict__ done) {
+                                         const double *cst, const double *fpv, const double *fpr, double ret_prev,
+                                         double bess0, double *__restrict__ reward, uint8_t *__restrict__ done) {
     // no global loads in here: a load would wait (vmcnt) for every SoC store the env just issued
-    const double solar = p.pv ? cst[CST_PV] * ratio : 0.0;         // central_management_system.py:99-103
+    const double solar = p.pv ? (cst[CST_PV] * ratio) * fpv[0] : 0.0;   // central_management_system.py:99-103
     const double demand = p_ch + p_dis;                            // :105
     if (demand < 0.0) fl |= p.v2x ? SNG_FLAG_V2X_BREAKPOINT : SNG_FLAG_NEGATIVE_DEMAND;
     double rem = demand - solar;                                   // :167
@@ -405,14 +441,14 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
 
     const double grid = rem;
     const double energy = grid * p.dt;
-    const double price = cst[CST_PRICE];
+    const double price = cst[CST_PRICE] * fpr[0];
     const double cost = (energy < 0.0) ? (energy * p.sell_coef) * price : energy * price;
     const double tot_pen = p.bat_pen_w * pen_b + pen_v;
     const double total = p.grid_w * fabs(cost) + tot_pen;
     SNG_ST(reward[e], -total);
     SNG_ST(done[e], (uint8_t)((t + 1 == p.T) ? 1 : 0));
 
-    write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio);
+    write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio, fpv, fpr);
     if (p.bess) o_row[p.obs_dim - 1] = (float)bess;
 
     if (fl) atomicOr(&s.flags[e], fl);   // rare (sticky error bits); no-return atomic, nothing waits
@@ -552,8 +588,18 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     const double bess = p.bess ? bess_l : 0.0;
     const double pen0 = (t == 0) ? pen0_l : 0.0;
     const double ret_prev = info.episode_return ? ret_l : 0.0;
-    // 2. requested SoC of the first batch (uniform branch, ahead of the tile)
+    // 2. requested SoC of the first batch and the day's profile factors for t..t+3 (uniform
+    //    branches, ahead of the tile)
     load_req(cbeg);
+    double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
+    if (p.noise) {
+        const size_t plane = (size_t)(p.T + 3) * E;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            fpv[j] = s.prof[(size_t)(t + j) * E + el];
+            fpr[j] = s.prof[plane + (size_t)(t + j) * E + el];
+        }
+    }
     // 3. tables and the actions tile
     constexpr int RCP_PER_THREAD = 256 / BLOCK;
     double rcp_v[RCP_PER_THREAD];
@@ -672,7 +718,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         }
         env_tail<DIAG>(p, s, info, e, t, ratio, bess, p.bess ? a_row[n] : 0.0f, p_ch, p_dis, pen_v,
                        100.0 * (double)n_nonexist, fl,
-                       o_row, s_cst, ret_prev, bess0, reward, done);
+                       o_row, s_cst, fpv, fpr, ret_prev, bess0, reward, done);
     }
     __syncthreads();
     SNG_STAMP(2);
@@ -696,7 +742,16 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
     float *o_row = lds + tid * O;
     if (tid < nblk) {
         const double ratio = s.ratio[e];
-        write_obs_header(o_row, p, s.tables->irr_norm, s.tables->price_norm, ratio);
+        double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
+        if (p.noise) {
+            const size_t plane = (size_t)(p.T + 3) * E;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                fpv[j] = s.prof[(size_t)j * E + e];
+                fpr[j] = s.prof[plane + (size_t)j * E + e];
+            }
+        }
+        write_obs_header(o_row, p, s.tables->irr_norm, s.tables->price_norm, ratio, fpv, fpr);
         const int k = p.pv ? 8 : 4;
         for (int c = 0; c < n; ++c) {
             const size_t idx = (size_t)c * E + e;   // t = 0 slice
@@ -714,6 +769,25 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
 }
 
 // ---------------------------------------------------------------------------------
+// Stochastic PV / price profiles of the day (build-defined, SngConfig.pv_noise / price_noise):
+// prof[0][k][e] = PV factor, prof[1][k][e] = price factor, k in [0, T + 3).  Runs in every reset
+// before observe0_kernel, which advances the day counter it reads.  Thread = env.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void profile_kernel(Params p, DeviceState s, int64_t E) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    const uint64_t day = *s.episode;
+    const uint64_t env_seed = p.seed + (uint64_t)p.env_offset + (uint64_t)e;
+    const int K = p.T + 3;
+    const size_t plane = (size_t)K * E;
+    for (int k = 0; k < K; ++k) {
+        s.prof[(size_t)k * E + e] = p.pv_noise != 0.0 ? profile_factor(env_seed, kDomainPV, day, k, p.pv_noise) : 1.0;
+        s.prof[plane + (size_t)k * E + e] =
+            p.price_noise != 0.0 ? profile_factor(env_seed, kDomainPrice, day, k, p.price_noise) : 1.0;
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // Device RNG day generator: the reference's per-charger vehicle process
 // (charging_station.py:200-279: arrival with p = 0.4 when the charger is free, arrival SoC
 // U(0.1, 0.9), capacity U{15..119}, requested SoC, departure U{t+4/dt .. min(t+10/dt, T+1/dt)-1})
@@ -722,30 +796,12 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
 // streams cost ~4x the VALU; the kernel is bound by its dense timeline stores otherwise).
 // Thread = (env, charger); writes the dense word / aux (/ req) timeline.
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {   // "triple32" integer hash (bijective)
-    x ^= x >> 17;
-    x *= 0xed5ad4bbu;
-    x ^= x >> 11;
-    x *= 0xac4c1b51u;
-    x ^= x >> 15;
-    x *= 0x31848babu;
-    x ^= x >> 14;
-    return x;
-}
-
 struct HashStream {
     uint32_t key, ctr;
     __device__ __forceinline__ uint32_t next() { return mix32(key + (ctr++) * 0x9e3779b9u); }
 };
 
 __device__ __forceinline__ double u32_unit(uint32_t x) { return (double)x * 0x1.0p-32; }   // [0, 1)
-
-// Stream key of (seed, global env, charger | domain, day).
-__device__ __forceinline__ uint32_t stream_key(uint64_t seed, uint64_t ge, uint32_t lane, uint64_t day) {
-    const uint32_t k0 = mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + (uint32_t)day * 0x9e3779b9u));
-    const uint32_t k1 = mix32(k0 ^ (uint32_t)ge);
-    return mix32(k1 ^ ((uint32_t)(ge >> 32) * 0x85ebca6bu + lane * 0xc2b2ae35u + 0x27d4eb2fu));
-}
 
 __device__ __forceinline__ int below(uint32_t x, int n) {   // floor(x * n / 2^32)
     return (int)(((uint64_t)x * (uint64_t)n) >> 32);
@@ -914,6 +970,13 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
                            hipStream_t stream) {
     const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)p.n), block(kGenBlock);
     hipLaunchKernelGGL(generate_kernel, grid, block, 0, stream, p, s, seed, E, i4, i10, i1);
+    return hipGetLastError();
+}
+
+hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream) {
+    if (!p.noise) return hipSuccess;
+    const dim3 grid((unsigned)((E + 255) / 256)), block(256);
+    hipLaunchKernelGGL(profile_kernel, grid, block, 0, stream, p, s, E);
     return hipGetLastError();
 }
 

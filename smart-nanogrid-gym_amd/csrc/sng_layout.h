@@ -43,7 +43,7 @@ constexpr int W_DEP_SHIFT = 16;
 constexpr int kMaxChargers = 128;   // numpy pairwise sum restated for n <= 128 (single level)
 constexpr int kSlots = 25;          // charger.py:16-19
 constexpr int kMaxT = 128;
-constexpr int kPriceLen = 48;       // accountant.py:201, 236
+constexpr int kPriceLen = 48;       // accountant.py:201, 236 (2T with the extended day)
 
 SNG_HD inline uint32_t pack_word(bool occ, bool stat, bool pen, uint32_t cap, uint32_t dep) {
     return (occ ? W_OCC : 0u) | (stat ? W_STATIC : 0u) | (pen ? W_PEN : 0u) | ((cap & 0xffu) << W_CAP_SHIFT) |
@@ -54,8 +54,8 @@ SNG_HD inline uint32_t pack_word(bool occ, bool stat, bool pen, uint32_t cap, ui
 struct Tables {
     double irr_norm[4 * kMaxT];    // irr[k] / irr_max          (pv_system_manager.py:369-373)
     double pv_power[4 * kMaxT];    // available_solar_power[k]  (:375-379)
-    double price[kPriceLen];       // energy_price[0, k]        (accountant.py:225-227)
-    double price_norm[kPriceLen];  // energy_price / max        (:229-233)
+    double price[4 * kMaxT];       // energy_price[0, k]        (accountant.py:225-227)
+    double price_norm[4 * kMaxT];  // energy_price / max        (:229-233)
     double recip[256];             // 1.0 / c (correctly rounded), c = vehicle capacity; recip[0] = 0
     int32_t n_irr;
 };
@@ -77,6 +77,9 @@ struct Params {
     double grid_w, bat_pen_w, sell_coef;
     int64_t env_offset;       // global index of env 0 of this handle (sharded runs)
     int32_t lanes;            // step kernel: lanes per environment (1, 2 or 4)
+    int32_t noise;            // 1: stochastic PV / price profiles (DeviceState::prof is live)
+    double pv_noise, price_noise;
+    uint64_t seed;            // handle seed: env e's seed is seed + env_offset + e
 };
 
 struct DeviceState {
@@ -84,6 +87,8 @@ struct DeviceState {
     uint32_t *word;
     double *aux, *req;
     uint32_t *flags;
+    // profile factors of the current day, [2][T + 3][E] (PV, price), only when Params::noise
+    double *prof;
     uint64_t *episode;        // device-side day counter for the device generator
     const Tables *tables;
 };

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SNG_LIBRARY", os.path.join(os.path.dirname(PKG_DIR), 
 DATA_DIR = os.path.join(PKG_DIR, "data")
 IRRADIANCE_FILE = os.path.join(DATA_DIR, "solar_irradiance_1min.f64")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 SNG_OK = 0
 RNG_REFERENCE = 0
 RNG_DEVICE = 1
@@ -62,13 +62,17 @@ class SngConfig(ctypes.Structure):
         ("irradiance_per_minute", c_double_p),
         ("irradiance_minutes", ctypes.c_int64),
         ("step_lanes_per_env", ctypes.c_int32),
+        ("extended_day", ctypes.c_int32),
+        ("reserved0", ctypes.c_int32),
+        ("pv_noise", ctypes.c_double),
+        ("price_noise", ctypes.c_double),
     ]
 
 
 class SngDims(ctypes.Structure):
     _fields_ = [("obs_dim", ctypes.c_int32), ("act_dim", ctypes.c_int32), ("timesteps", ctypes.c_int32),
                 ("number_of_chargers", ctypes.c_int32), ("num_envs", ctypes.c_int64),
-                ("step_lanes_per_env", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("step_lanes_per_env", ctypes.c_int32), ("slots", ctypes.c_int32)]
 
 
 INFO_FIELDS = ["grid_power", "total_charging_power", "total_discharging_power", "battery_state_of_charge",

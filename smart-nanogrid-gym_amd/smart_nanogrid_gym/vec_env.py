@@ -68,6 +68,7 @@ class SmartNanogridVecEnv:
         check(lib().sng_get_dims(h, ctypes.byref(dims)), h)
         self.obs_dim, self.act_dim, self.timesteps = dims.obs_dim, dims.act_dim, dims.timesteps
         self.step_lanes = dims.step_lanes_per_env
+        self.slots = dims.slots
         E = self.num_envs
         dev = self.device
         self.actions_d = torch.zeros((E, self.act_dim), dtype=torch.float32, device=dev)
@@ -155,10 +156,11 @@ class SmartNanogridVecEnv:
         if len(items) != E:
             raise ValueError("need one initial_values dict per env")
         V = max(1, max(len(a) for d in items for a in d["Arrivals"]))
-        soc = np.zeros((E, N, SLOTS))
-        occ = np.zeros((E, N, SLOTS))
-        cap = np.zeros((E, N, SLOTS))
-        req = np.zeros((E, N, SLOTS))
+        S = self.slots
+        soc = np.zeros((E, N, S))
+        occ = np.zeros((E, N, S))
+        cap = np.zeros((E, N, S))
+        req = np.zeros((E, N, S))
         arr = np.full((E, N, V), -1, np.int32)
         dep = np.full((E, N, V), -1, np.int32)
         for i, d in enumerate(items):
@@ -174,14 +176,17 @@ class SmartNanogridVecEnv:
         return self.reset_from_arrays(soc, occ, cap, req, arr, dep, ratio)
 
     def reset_from_arrays(self, soc, occupancy, capacity, requested_soc, arrivals, departures, pv_ratio):
-        """Start a day from explicit reference-layout arrays ([E, N, 25] / [E, N, V], -1 padded)."""
+        """Start a day from explicit reference-layout arrays ([E, N, slots] / [E, N, V], -1 padded;
+        slots = 25, or T+1 with the build-defined extended day)."""
         self._check_mode()
         arrs = [np.ascontiguousarray(a, np.float64) for a in (soc, occupancy, capacity, requested_soc)]
         ai = np.ascontiguousarray(arrivals, np.int32)
         di = np.ascontiguousarray(departures, np.int32)
         ratio = np.ascontiguousarray(pv_ratio, np.float64)
         sc = _native.SngScenario()
-        sc.slots = SLOTS
+        if arrs[0].shape[-1] != self.slots:
+            raise ValueError(f"scenario arrays need {self.slots} slots per charger")
+        sc.slots = self.slots
         sc.max_vehicles = ai.shape[-1]
         sc.soc, sc.occupancy, sc.capacity, sc.requested_soc = [a.ctypes.data_as(_native.c_double_p) for a in arrs]
         sc.arrivals = ai.ctypes.data_as(_native.c_int32_p)

@@ -288,3 +288,59 @@ def test_sharded_population_reproduces_single_gpu(rng):
         assert torch.equal(full.return_d, torch.cat([h.return_d for h in halves]))
     for v in [full] + halves:
         v.close()
+
+
+CONFIG5 = dict(number_of_chargers=50, time_interval="15min", charging_mode="bounded",
+               vehicle_uncharged_penalty_mode="sparse", extended_day=True, pv_noise=0.2, price_noise=0.1)
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_config5_extended_day_stochastic_profiles_vs_oracle(lanes):
+    """BASELINE config 5 (50 chargers x 96 15-min steps, stochastic PV + price profiles), a
+    build-defined generalisation with no reference oracle: bit-exact against the oracle's
+    restatement of the same generalisation, reference RNG, two consecutive days."""
+    E, seed = 192, 55
+    O.lib().orc_set_square_mode(1)
+    venv = SmartNanogridVecEnv(E, seed=seed, rng="reference", step_lanes_per_env=lanes, **CONFIG5)
+    assert venv.timesteps == 96 and venv.slots == 97
+    cfg, envs = _oracle_batch(CONFIG5, seed, range(E))
+    rng = np.random.default_rng(17)
+    obs = venv.reset()
+    np.testing.assert_array_equal(obs, np.stack([e.reset() for e in envs]))
+    for day in range(2):
+        if day > 0:
+            np.testing.assert_array_equal(obs, np.stack([e.reset() for e in envs]))
+        for t in range(cfg.T):
+            a = rng.uniform(venv.action_space.low, venv.action_space.high, (E, venv.act_dim)).astype(np.float32)
+            a[rng.random(a.shape) < 0.2] = 0
+            obs, rew, dones, infos = venv.step(a)
+            outs = [e.step(a[i]) for i, e in enumerate(envs)]
+            got = np.stack([inf.get("terminal_observation", obs[i]) for i, inf in enumerate(infos)])
+            np.testing.assert_array_equal(got, np.stack([o[0] for o in outs]), err_msg=f"day{day} t{t}")
+            np.testing.assert_array_equal(rew, np.array([o[1] for o in outs]))
+            assert dones.all() == (t == cfg.T - 1)
+    venv.close()
+
+
+def test_config5_full_size_device_rng_day():
+    """Config 5 at its full size (65,536 envs x 50 chargers x 96 steps) with GPU-generated days:
+    a graph-replayed day equals the eager day bit for bit, and size-independent invariants hold."""
+    E = 65536
+    acts = torch.rand((96, E, 51), device="cuda:0")
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    a = SmartNanogridVecEnv(E, seed=3, rng="device", info=True, **CONFIG5)
+    b = SmartNanogridVecEnv(E, seed=3, rng="device", **CONFIG5)
+    graph = EpisodeGraph(b, acts)
+    a.reset_tensors()
+    for t in range(96):
+        o, r, dn = a.step_tensors(acts[t])
+        soc = o[:, 8:58]
+        assert bool(torch.isfinite(r).all()) and bool((r <= 0).all())
+        assert float(soc.min()) >= 0 and float(soc.max()) <= 1
+        assert (a.last_info()["flags"] == 0).all()
+    graph.launch()
+    torch.cuda.synchronize()
+    assert torch.equal(o, b.obs_d) and torch.equal(r, b.reward_d) and torch.equal(a.return_d, b.return_d)
+    graph.close()
+    a.close()
+    b.close()

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_native.EXPORTS), "ctypes binding out of sync with include/sng.h"
-    assert L.sng_abi_version() == 2
+    assert L.sng_abi_version() == 3
 
 
 def test_config_defaults_are_reference_constants():
@@ -61,7 +61,8 @@ def host_days(kwargs, n_envs, seed, episodes, V=8):
     s = EnvSettings(**kwargs)
     cfg = s.to_native()
     N = s.number_of_chargers
-    shp = (episodes, n_envs, N, 25)
+    S = s.timesteps + 1 if kwargs.get("extended_day") else 25
+    shp = (episodes, n_envs, N, S)
     soc, occ, cap, req = (np.zeros(shp) for _ in range(4))
     arr = np.zeros((episodes, n_envs, N, V), np.int32)
     dep = np.zeros((episodes, n_envs, N, V), np.int32)
@@ -102,3 +103,59 @@ def test_host_generator_matches_oracle_many_seeds():
             assert days["ratio"][ep, i] == env.ratio
             for t in range(cfg.T):   # advance the oracle through the day (consumes the day-end draw)
                 env.step(np.zeros(cfg.act_dim, np.float32))
+
+
+CONFIG5 = dict(number_of_chargers=50, time_interval="15min", charging_mode="bounded",
+               vehicle_uncharged_penalty_mode="sparse", extended_day=True, pv_noise=0.2, price_noise=0.1)
+
+
+def test_extended_day_host_generator_matches_oracle():
+    """Build-defined extended day (N=50, 15 min, T=96, T+1 slots): the
+    library's host generator and the oracle draw the same days from the reference's streams."""
+    E, seed = 24, 4242
+    days = host_days(CONFIG5, E, seed, 2)
+    assert days["soc"].shape[-1] == 97
+    cfg = O.OracleConfig(**CONFIG5)
+    assert cfg.T == 96 and cfg.slots == 97
+    for i in range(0, E, 5):
+        env = O.OracleEnv(cfg, seed + i)
+        for ep in range(2):
+            env.reset()
+            sc = env.scenario(vmax=8)
+            for k in ["soc", "occ", "cap", "req", "arrivals", "departures"]:
+                np.testing.assert_array_equal(days[k][ep, i], sc[k])
+            assert days["ratio"][ep, i] == env.ratio
+            for t in range(cfg.T):
+                env.step(np.zeros(cfg.act_dim, np.float32))
+
+
+def test_extended_day_tables_and_profiles():
+    cfg = O.OracleConfig(**CONFIG5)
+    tb = cfg.tables()
+    assert tb["price"].size == 192 and tb["irr"].size == 192
+    low, high = tb["price"].min(), tb["price"].max()
+    # per-step tariff loop (accountant.py:61-68): low for i < 7/dt or i > 19/dt
+    for i in range(96):
+        assert tb["price"][i] == (low if (i < 28 or i > 76) else high)
+        assert tb["price"][i + 96] == tb["price"][i]
+    env = O.OracleEnv(cfg, 5)
+    env.reset()
+    f1 = env.profiles()
+    env.reset()
+    f2 = env.profiles()
+    for (pv, pr), (pv2, pr2) in [(f1, f2)]:
+        assert pv.size == 99 and np.all(np.abs(pv - 1) <= 0.2) and np.all(np.abs(pr - 1) <= 0.1)
+        assert not np.array_equal(pv, pv2)   # a new day draws new profiles
+    # standard configs keep the reference's 25 slots and refuse T > 24
+    with pytest.raises(IndexError):
+        O.OracleEnv(O.OracleConfig(number_of_chargers=2, time_interval="15min"), 0)
+
+
+def test_create_rejects_extended_day_without_flag():
+    kw = dict(CONFIG5)
+    kw.pop("extended_day")
+    s = EnvSettings(**kw)
+    cfg = s.to_native()
+    h = ctypes.c_void_p()
+    rc = _native.lib().sng_create(ctypes.byref(cfg), 0, 4, 0, ctypes.byref(h))
+    assert rc != 0 and b"extended_day" in _native.lib().sng_last_error(None)
