@@ -32,18 +32,18 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "env-steps/sec (whole node) at N=65,536 envs × 10 chargers, 24-step day"
 
 
-def step_kernel_bytes(n):
+def step_kernel_bytes(n, noise=False):
     """Algorithmic bytes one env moves in one fused step (b-pv, no requested-SoC stream):
     actions 4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N + scenario word 4N
-    + static SoC 8N + BESS r/w 16 + PV ratio 8 + day-return r/w 16 = 40N + 89."""
-    return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 4 * n + 8 * n + 16 + 8 + 16
+    + static SoC 8N + BESS r/w 16 + PV ratio 8 + day-return r/w 16 = 40N + 89
+    (+ 64 for the PV / price profile factors of t..t+3 with stochastic profiles)."""
+    return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 4 * n + 8 * n + 16 + 8 + 16 + (64 if noise else 0)
 
 
-def cpu_baseline(chargers, budget_s):
+def cpu_baseline(kw, budget_s):
     import oracle as O
-    kw = dict(number_of_chargers=chargers, time_interval="1h", charging_mode="bounded",
-              vehicle_uncharged_penalty_mode="sparse")
     cfg = O.OracleConfig(**kw)
+    chargers = cfg.N
     A = cfg.act_dim
     batch = 256
     rng = np.random.default_rng(0)
@@ -57,7 +57,8 @@ def cpu_baseline(chargers, budget_s):
         envs += batch
     dt = time.perf_counter() - t0
     return {"value": envs * cfg.T / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{envs} envs x 1 day (reset + 24 steps each), b-pv N={chargers} sparse 1h, "
+            "sample": f"{envs} envs x 1 day (reset + {cfg.T} steps each), b-pv N={chargers} sparse "
+                      f"{kw.get('time_interval', '1h')}, "
                       f"C oracle (scalar restatement of the reference) on 1 host thread, {dt:.1f} s"}
 
 
@@ -83,6 +84,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--chargers", type=int, default=10)
+    ap.add_argument("--time-interval", default="1h", help="'15min' with --extended-day = BASELINE config 5")
+    ap.add_argument("--extended-day", action="store_true", help="build-defined days longer than 24 steps")
+    ap.add_argument("--pv-noise", type=float, default=0.0, help="stochastic PV profile sigma (config 5: 0.2)")
+    ap.add_argument("--price-noise", type=float, default=0.0, help="stochastic price profile sigma (config 5: 0.1)")
     ap.add_argument("--lanes", type=int, default=0, help="step kernel lanes per env (0 = library default)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-budget", type=float, default=12.0)
@@ -105,9 +110,12 @@ def main():
     from smart_nanogrid_gym.parallel import max_over_ranks, shard_envs
 
     E, N = args.envs, args.chargers
-    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+    kw = dict(number_of_chargers=N, time_interval=args.time_interval, charging_mode="bounded",
               vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
               battery_system_available_in_model=True)
+    noise = args.pv_noise > 0 or args.price_noise > 0
+    if args.extended_day or noise:
+        kw.update(extended_day=args.extended_day, pv_noise=args.pv_noise, price_noise=args.price_noise)
     offset, _ = shard_envs(world * E, world, rank)   # weak scaling: E envs per GPU, global ids
     venv = SmartNanogridVecEnv(E, seed=args.seed, device=local, rng="device", env_offset=offset,
                                step_lanes_per_env=args.lanes, **kw)
@@ -156,19 +164,23 @@ def main():
         env_steps = world * E * T * args.steps
         value = env_steps / elapsed
         launch_s = float(np.mean(kernel_ms)) / 1e3
-        bpl = step_kernel_bytes(N) * E
+        bpl = step_kernel_bytes(N, noise) * E
         achieved = bpl / launch_s / 1e9
         kernel = f"void sng::step_kernel<{N}, {venv.step_lanes}, false, true>"
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N, kernel),
                 "kernel": kernel, "bytes_per_launch": bpl,
                 "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src}
-        cpu = None if args.no_cpu_baseline else cpu_baseline(N, args.cpu_budget)
-        out = {"metric": METRIC, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
+        cpu = None if args.no_cpu_baseline else cpu_baseline(kw, args.cpu_budget)
+        headline = (N == 10 and T == 24 and not noise)
+        metric = METRIC if headline else f"env-steps/sec (whole node) at N={E:,} envs × {N} chargers, {T}-step day"
+        desc = f"b-pv bounded sparse {args.time_interval}" + (
+            f", extended day, stochastic PV/price profiles (sigma {args.pv_noise}/{args.price_noise})" if not headline else "")
+        out = {"metric": metric, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-               "config": {"workload": f"{E} envs/GPU x {N} chargers x {T}-step day, b-pv bounded sparse 1h, "
-                                      "GPU-RNG reset + 24 fused steps per bench step (hipGraph)",
+               "config": {"workload": f"{E} envs/GPU x {N} chargers x {T}-step day, {desc}, "
+                                      f"GPU-RNG reset + {T} fused steps per bench step (hipGraph)",
                           "envs_per_gpu": E, "chargers": N, "timesteps": T,
                           "step_unit": "one simulated day of every env",
                           "parallelism": f"env-sharded x{world}" + (", RCCL all-gather of day returns" if world > 1 else "")},
