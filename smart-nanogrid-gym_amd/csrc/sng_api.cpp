@@ -582,7 +582,9 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
         }
         p.lanes = c.step_lanes_per_env;
     } else {
-        p.lanes = 1;   // tuned on MI355X at N=10, E=65,536 (tools/gpu_session.sh sweep)
+        // tuned on MI355X at E=65,536: 1 lane at N=10 (tools/gpu_session.sh sweep), 2 at N=50
+        // (74 vs 96 us per step, profiles/r01_bench_config5*.log)
+        p.lanes = (p.n > 16 && step_lanes_supported(p.n, 2)) ? 2 : 1;
     }
     env->i4 = (int)(4 / p.dt);
     env->i10 = (int)(10 / p.dt);

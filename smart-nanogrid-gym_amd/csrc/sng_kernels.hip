@@ -798,7 +798,11 @@ __global__ __launch_bounds__(256) void profile_kernel(Params p, DeviceState s, i
 // ---------------------------------------------------------------------------------
 struct HashStream {
     uint32_t key, ctr;
+#ifdef SNG_GEN_CHEAP   // diagnostic build only: no hashing (timing floor of the generator's stores)
+    __device__ __forceinline__ uint32_t next() { return key ^ ((ctr++) * 0x9e3779b9u); }
+#else
     __device__ __forceinline__ uint32_t next() { return mix32(key + (ctr++) * 0x9e3779b9u); }
+#endif
 };
 
 __device__ __forceinline__ double u32_unit(uint32_t x) { return (double)x * 0x1.0p-32; }   // [0, 1)

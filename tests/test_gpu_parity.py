@@ -344,3 +344,28 @@ def test_config5_full_size_device_rng_day():
     graph.close()
     a.close()
     b.close()
+
+
+@pytest.mark.parametrize("E,N", [(1000, 10), (515, 50), (333, 7)])
+def test_unaligned_actions_take_the_scalar_staging_path(E, N):
+    """Actions at a 4-byte (not 16-byte) aligned address switch the LDS staging to its scalar
+    path; results are identical to the aligned run, including ragged last workgroups."""
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="dense")
+    a = SmartNanogridVecEnv(E, seed=21, rng="reference", **kw)
+    b = SmartNanogridVecEnv(E, seed=21, rng="reference", **kw)
+    A = a.act_dim
+    oa, ob = a.reset_tensors().clone(), b.reset_tensors().clone()
+    assert torch.equal(oa, ob)
+    g = torch.Generator(device="cuda:0").manual_seed(4)
+    buf = torch.empty(E * A + 1, device="cuda:0")
+    for t in range(a.timesteps):
+        acts = torch.rand((E, A), generator=g, device="cuda:0")
+        unaligned = buf[1:].view(E, A)
+        unaligned.copy_(acts)
+        assert unaligned.data_ptr() % 16 != 0 and unaligned.is_contiguous()
+        oa, ra, da = a.step_tensors(acts)
+        ob, rb, db = b.step_tensors(unaligned)
+        assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db)
+    a.close()
+    b.close()
