@@ -753,12 +753,28 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
         }
         write_obs_header(o_row, p, s.tables->irr_norm, s.tables->price_norm, ratio, fpv, fpr);
         const int k = p.pv ? 8 : 4;
-        for (int c = 0; c < n; ++c) {
-            const size_t idx = (size_t)c * E + e;   // t = 0 slice
-            const double aux = s.aux[idx];
-            s.soc[idx] = aux;
-            o_row[k + c] = (float)aux;
-            o_row[k + n + c] = departure_obs(s.word[idx]);
+        const uint32_t *__restrict__ word = s.word;
+        const double *__restrict__ auxv = s.aux;
+        double *__restrict__ socv = s.soc;
+        // batches of 8 chargers: all loads of a batch issued before its stores (t = 0 slice)
+        for (int c0 = 0; c0 < n; c0 += 8) {
+            uint32_t w[8];
+            double aux[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = c0 + j < n ? c0 + j : n - 1;
+                w[j] = word[(size_t)c * E + e];
+                aux[j] = auxv[(size_t)c * E + e];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int c = c0 + j;
+                if (c < n) {
+                    SNG_ST(socv[(size_t)c * E + e], aux[j]);
+                    o_row[k + c] = (float)aux[j];
+                    o_row[k + n + c] = departure_obs(w[j]);
+                }
+            }
         }
         if (p.bess) o_row[O - 1] = (float)s.bess[e];
         if (ep_return) ep_return[e] = 0.0;
