@@ -476,23 +476,37 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
 // so the [ENVS][O] observation tile stays well inside the 160 KB LDS.
 __host__ __device__ constexpr int step_block(int NC) { return (NC > 0 && NC <= 16) ? 256 : 64; }
 
-// LDS carve-up of the step kernel (every region 16-byte aligned):
-//   act [ENVS][A] f32 | obs [ENVS][O] f32 | rcp [256] f64 | cst [16] f64 | pos [ENVS][NC] f64 | neg [ENVS][NC] f64
-//   | (L > 1) pw [ENVS][NC] f64 | q [ENVS][NC] f64
+// LDS carve-up of the step kernel, one slice per wavefront (every region 16-byte aligned):
+//   act [WENVS][A] f32 | obs [WENVS][O] f32 | rcp [256] f64 | cst [16] f64
+//   | pos [WENVS][NC] f64 | neg [WENVS][NC] f64 | (L > 1) pw [WENVS][NC] f64 | q [WENVS][NC] f64
+// Each wavefront stages, computes and writes back its own 64/L envs: no workgroup barrier, so
+// the waves of a CU drift apart and one wave's loads overlap another's arithmetic and stores.
 template <int NC, int L>
 struct StepLds {
     static constexpr int BLOCK = step_block(NC);
-    static constexpr int ENVS = BLOCK / L;
+    static constexpr int WAVES = BLOCK / kWave;
+    static constexpr int WENVS = kWave / L;             // envs per wavefront
+    static constexpr int ENVS = BLOCK / L;               // envs per workgroup
     static constexpr bool kRows = NC > 0 && NC <= 16;   // compacted power rows (else PairwiseSum)
-    __host__ __device__ static int act_floats(int A) { return round4(ENVS * A); }
-    __host__ __device__ static int obs_floats(int O) { return round4(ENVS * O); }
-    __host__ __device__ static size_t bytes(int A, int O) {
+    __host__ __device__ static int act_floats(int A) { return round4(WENVS * A); }
+    __host__ __device__ static int obs_floats(int O) { return round4(WENVS * O); }
+    __host__ __device__ static size_t wave_bytes(int A, int O) {
         size_t b = (size_t)(act_floats(A) + obs_floats(O)) * 4 + (256 + 16) * 8;
-        if (kRows) b += (size_t)2 * ENVS * NC * 8;
-        if (L > 1) b += (size_t)2 * ENVS * NC * 8;
+        if (kRows) b += (size_t)2 * WENVS * NC * 8;
+        if (L > 1) b += (size_t)2 * WENVS * NC * 8;
         return b;
     }
+    __host__ __device__ static size_t bytes(int A, int O) { return WAVES * wave_bytes(A, O); }
 };
+
+// LDS ordering inside one wavefront: a wave's LDS operations complete in issue order, so a
+// compiler-level fence is all that is needed between the writes of some lanes and the reads of
+// others (no s_barrier).
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // ---------------------------------------------------------------------------------
 // The fused step: SmartNanogridEnv.step(actions) for BLOCK/L envs per workgroup.
@@ -509,28 +523,30 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                                                               int64_t E, int t, int vec_io) {
     static_assert(L == 1 || NC > 0, "multi-lane envs need a compile-time charger count");
     using Lay = StepLds<NC, L>;
-    constexpr int BLOCK = Lay::BLOCK;
-    constexpr int ENVS = Lay::ENVS;
+    constexpr int WENVS = Lay::WENVS;
     constexpr bool kRows = Lay::kRows;
     constexpr int CH = (L > 1) ? (NC + L - 1) / L : ((NC > 0 && NC <= 16) ? NC : 8);
+    // actions tile in one round: K float4 per lane covers WENVS * A floats for A <= NC + 1
+    constexpr int KT = NC > 0 ? ((NC + 1) * WENVS + 4 * kWave - 1) / (4 * kWave) : 8;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int n = NC ? NC : p.n;
     const int A = p.act_dim, O = p.obs_dim;
-    const int tid = threadIdx.x;
-    const int le = tid / L, part = tid % L;
-    const int64_t e0 = (int64_t)blockIdx.x * ENVS;
-    const int nblk = (int)((E - e0) < ENVS ? (E - e0) : ENVS);
+    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    const int le = lane / L, part = lane % L;
+    const int64_t e0 = (int64_t)blockIdx.x * Lay::ENVS + (int64_t)wave * WENVS;   // this wave's first env
+    if (e0 >= E) return;                                                           // wave-uniform
+    const int nw = (int)((E - e0) < WENVS ? (E - e0) : WENVS);
     const int64_t e = e0 + le;
-    const bool live = le < nblk;
+    const bool live = le < nw;
     const bool leader = part == 0;
-    float *s_act = lds;
-    float *s_obs = lds + Lay::act_floats(A);
+    float *s_act = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + wave * Lay::wave_bytes(A, O));
+    float *s_obs = s_act + Lay::act_floats(A);
     double *s_rcp = reinterpret_cast<double *>(s_obs + Lay::obs_floats(O));
     double *s_cst = s_rcp + 256;                                  // [16] per-step constants (CST_*)
-    double *s_pos = s_cst + 16;                                   // [ENVS][NC] compacted positive powers
-    double *s_neg = s_pos + (kRows ? ENVS * NC : 0);              // [ENVS][NC] compacted negative powers
-    double *s_pw = s_neg + (kRows ? ENVS * NC : 0);               // [ENVS][NC] per-charger powers (L > 1)
-    double *s_q = s_pw + (L > 1 ? ENVS * NC : 0);                 // [ENVS][NC] per-charger penalty terms
+    double *s_pos = s_cst + 16;                                   // [WENVS][NC] compacted positive powers
+    double *s_neg = s_pos + (kRows ? WENVS * NC : 0);             // [WENVS][NC] compacted negative powers
+    double *s_pw = s_neg + (kRows ? WENVS * NC : 0);              // [WENVS][NC] per-charger powers (L > 1)
+    double *s_q = s_pw + (L > 1 ? WENVS * NC : 0);                // [WENVS][NC] per-charger penalty terms
     const uint32_t *__restrict__ word = s.word;
     const double *__restrict__ auxv = s.aux;
     const double *__restrict__ reqv = s.req;
@@ -539,9 +555,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     const int cbeg = (L > 1) ? part * CH : 0;
     const int cend = (L > 1) ? ((cbeg + CH) < n ? (cbeg + CH) : n) : n;
 
-    // Loads are issued oldest-needed-last: everything the block barrier waits for (tables,
-    // actions tile) is issued after the conditional loads and before the per-charger state, and
-    // no branch separates it from the per-charger loads, so the wait before the LDS commits is
+    // Loads are issued oldest-needed-last: everything the LDS commits wait for (tables, actions
+    // tile) is issued after the conditional loads and before the per-charger state, and no
+    // branch separates it from the per-charger loads, so the wait before the commits is
     // vmcnt(#per-charger loads) and charger c's update starts as soon as its own loads land.
     // Non-live lanes load a valid env (E - 1) and discard it.
     const int64_t el = live ? e : E - 1;
@@ -600,24 +616,24 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             fpr[j] = s.prof[plane + (size_t)(t + j) * E + el];
         }
     }
-    // 3. tables and the actions tile
-    constexpr int RCP_PER_THREAD = 256 / BLOCK;
-    double rcp_v[RCP_PER_THREAD];
+    // 3. tables and the wave's actions tile
+    constexpr int RCP_PER_LANE = 256 / kWave;
+    double rcp_v[RCP_PER_LANE];
 #pragma unroll
-    for (int k = 0; k < RCP_PER_THREAD; ++k) rcp_v[k] = s.tables->recip[k * BLOCK + tid];
-    const double cst_v = (tid < CST_COUNT) ? step_constant(s.tables, t, tid) : 0.0;
-    TileStage<(NC > 0 && NC < 16) ? 4 : 8, BLOCK> act_tile;
-    act_tile.issue(act + e0 * A, nblk * A, vec_io != 0, tid);
+    for (int k = 0; k < RCP_PER_LANE; ++k) rcp_v[k] = s.tables->recip[k * kWave + lane];
+    const double cst_v = (lane < CST_COUNT) ? step_constant(s.tables, t, lane) : 0.0;
+    TileStage<KT, kWave> act_tile;
+    act_tile.issue(act + e0 * A, nw * A, vec_io != 0, lane);
     // 4. per-charger state of the first batch
     load_state(cbeg);
 #ifdef SNG_STAMPS
     if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
 #endif
 #pragma unroll
-    for (int k = 0; k < RCP_PER_THREAD; ++k) s_rcp[k * BLOCK + tid] = rcp_v[k];
-    if (tid < CST_COUNT) s_cst[tid] = cst_v;
-    act_tile.commit(s_act, tid);
-    __syncthreads();
+    for (int k = 0; k < RCP_PER_LANE; ++k) s_rcp[k * kWave + lane] = rcp_v[k];
+    if (lane < CST_COUNT) s_cst[lane] = cst_v;
+    act_tile.commit(s_act, lane);
+    wave_lds_fence();
     SNG_STAMP(1);
 
     const float *a_row = s_act + le * A;
@@ -688,14 +704,14 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         }
     }
     if (L > 1) {
-        // gather the env's lanes: counts and flag bits, then in-order
+        // gather the env's lanes (same wavefront): counts and flag bits, then in-order
         // penalty / power sums by the leader from LDS
 #pragma unroll
         for (int off = 1; off < L; off <<= 1) {
             n_nonexist += (uint32_t)__shfl_down((int)n_nonexist, off, L);
             fl |= (uint32_t)__shfl_down((int)fl, off, L);
         }
-        __syncthreads();
+        wave_lds_fence();
         if (live && leader) {
 #pragma unroll
             for (int c = 0; c < NC; ++c) {
@@ -720,9 +736,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                        100.0 * (double)n_nonexist, fl,
                        o_row, s_cst, fpv, fpr, ret_prev, bess0, reward, done);
     }
-    __syncthreads();
+    wave_lds_fence();
     SNG_STAMP(2);
-    copy_out<BLOCK>(obs + e0 * O, s_obs, nblk * O, vec_io != 0, tid);
+    copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
     SNG_STAMP(3);
 }
 
