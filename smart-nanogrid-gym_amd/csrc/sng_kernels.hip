@@ -713,10 +713,27 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         }
         wave_lds_fence();
         if (live && leader) {
+            if (kRows) {
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                pen_v += s_q[le * NC + c];
-                add_power(s_pw[le * NC + c]);
+                for (int c = 0; c < NC; ++c) {
+                    pen_v += s_q[le * NC + c];
+                    add_power(s_pw[le * NC + c]);
+                }
+            } else {
+                // wide stations: compact in place -- positives into the power row, negatives into
+                // the penalty row; slot k <= c has been read before it is rewritten at step c
+                double *pw_row = s_pw + le * NC, *q_row = s_q + le * NC;
+#pragma unroll 10
+                for (int c = 0; c < NC; ++c) {
+                    const double qv = q_row[c], v = pw_row[c];
+                    pen_v += qv;
+                    pw_row[n_pos] = v;
+                    q_row[n_neg] = v;
+                    seq_pos += __builtin_fmax(v, 0.0);
+                    seq_neg += __builtin_fmin(v, 0.0);
+                    n_pos += (v > 0.0) ? 1 : 0;
+                    n_neg += (v < 0.0) ? 1 : 0;
+                }
             }
         }
     }
@@ -728,6 +745,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         if (kRows) {
             p_ch = pairwise_row(row_pos, n_pos, seq_pos);
             p_dis = pairwise_row(row_neg, n_neg, seq_neg);
+        } else if (L > 1) {
+            p_ch = pairwise_row(s_pw + le * NC, n_pos, seq_pos);
+            p_dis = pairwise_row(s_q + le * NC, n_neg, seq_neg);
         } else {
             p_ch = pos.result();
             p_dis = neg.result();
