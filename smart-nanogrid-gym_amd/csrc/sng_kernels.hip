@@ -890,12 +890,15 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
                 arrived = true;
                 present = true;
                 soc_arr = 0.1 + (0.9 - 0.1) * u32_unit(rng.next());       // uniform(0.1, 0.9)
+                // capacity and departure from one draw: cap = floor(y * 105 / 2^32); the low word of
+                // y * 105 (a bijection of y, uniform given cap) drives the departure
                 const uint32_t y = rng.next();
                 cap = p.diff_caps ? (uint32_t)(15 + below(y, 105)) : 40u;   // randint(15, 120)
+                const uint32_t yd = p.diff_caps ? y * 105u : y;
                 const int hi_c = t + i10, hi_d = T + i1;
                 const int high = hi_c < hi_d ? hi_c : hi_d;
                 const int low = t + i4;
-                dep = (low >= high) ? low : low + below(rng.next(), high - low);
+                dep = (low >= high) ? low : low + below(yd, high - low);
                 if (p.req_enabled) {
                     const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
                     req = lo + (1.0 - lo) * u32_unit(rng.next());
@@ -917,10 +920,12 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
             }
         }
         const int rem = occ ? dep - t : 0;
-        const size_t idx = ((size_t)t * n + c) * (size_t)E + e;
-        SNG_GST(s.word[idx], pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem));
-        SNG_GST(s.aux[idx], arrived ? soc_arr : 0.0);   // dense: full-line stores
-        if (p.req_stream) SNG_GST(s.req[idx], pen ? req : 0.0);
+        // row base is wave-uniform (scalar), the lane adds a 32-bit offset
+        const size_t row = ((size_t)t * n + c) * (size_t)E;
+        const uint32_t el = (uint32_t)e;
+        SNG_GST(s.word[row + el], pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem));
+        SNG_GST(s.aux[row + el], arrived ? soc_arr : 0.0);   // dense: full-line stores
+        if (p.req_stream) SNG_GST(s.req[row + el], pen ? req : 0.0);
         prev_occ = occ;
         prev_rem = rem;
     }
