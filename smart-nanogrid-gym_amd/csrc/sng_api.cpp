@@ -371,6 +371,10 @@ int fail(SngEnv *env, int code, const std::string &msg) {
     return code;
 }
 
+// The device generator keeps up to 8 vehicles per charger and day in LDS (sng_kernels.hip,
+// kDayVehicles): a vehicle stays >= 4/dt steps and leaves one step empty.
+bool device_rng_ok(const SngEnv *env) { return env->i4 >= 2 && env->p.T / (env->i4 + 1) + 1 <= 8; }
+
 int hip_fail(SngEnv *env, hipError_t e, const char *what) {
     return fail(env, SNG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
 }
@@ -702,7 +706,7 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     HIP_TRY(env, hipSetDevice(env->device));
     hipStream_t st = (hipStream_t)stream;
     if (rng_mode == SNG_RNG_DEVICE) {
-        if (env->i4 < 2) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
+        if (!device_rng_ok(env)) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
         env->p.req_stream = env->p.req_enabled;
         if (env->p.req_stream) {
             int rc = ensure_req(env);
@@ -879,7 +883,8 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
                      const SngInfo *info, int flags, SngGraph **out) {
     const bool with_reset = (flags & SNG_GRAPH_RESET) != 0;
     if (!env || !actions || !obs || !reward || !done || !out) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
-    if (with_reset && env->i4 < 2) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
+    if (with_reset && !device_rng_ok(env))
+        return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
     HIP_TRY(env, hipSetDevice(env->device));
     if (env->p.req_enabled) {
         int rc = ensure_req(env);
@@ -940,7 +945,7 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
                           const SngInfo *info, int32_t days, float *ms, void *stream) {
     if (!env || !actions || !obs || !reward || !done || !ms || days < 1)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
-    if (env->i4 < 2) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
+    if (!device_rng_ok(env)) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
     HIP_TRY(env, hipSetDevice(env->device));
     hipStream_t st = (hipStream_t)stream;
     Params p = env->p;

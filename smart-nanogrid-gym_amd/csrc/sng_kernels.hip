@@ -863,14 +863,32 @@ __device__ __forceinline__ int below(uint32_t x, int n) {   // floor(x * n / 2^3
     return (int)(((uint64_t)x * (uint64_t)n) >> 32);
 }
 
-// round(rand() - 0.1) == 1  <=>  rand() > 0.6: the 32-bit threshold ceil(0.6 * 2^32)
-constexpr uint32_t kArrivalThreshold = 2576980378u;
+// An arrival happens iff round(rand() - 0.1) == 1, i.e. rand() > 0.6 (p = 0.4) at each free step.
 
-constexpr int kGenBlock = 256;   // 4 waves of consecutive envs, same charger
+constexpr int kGenBlock = 256;       // 4 waves of consecutive envs, same charger
+// vehicles per charger and day: each stays >= 4/dt steps and leaves one empty step, so at most
+// T / (4/dt + 1) + 1 <= 7 (checked on the host); slots for 8
+constexpr int kDayVehicles = 8;
+constexpr float kInvLog2Q = -1.3569154488567239f;   // 1 / log2(0.6)
 
+__host__ __device__ constexpr size_t generate_lds_bytes(bool with_req) {
+    return (size_t)kDayVehicles * kGenBlock * (sizeof(uint32_t) + sizeof(double) + (with_req ? sizeof(double) : 0));
+}
+
+// Two phases per (env, charger):
+//  1. the day's vehicles: the waiting time to the next arrival is the number of failed
+//     Bernoulli(0.4) trials before the first success (geometric, one draw via -log2(u)/-log2(0.6)),
+//     then arrival SoC, capacity and departure -- a few draws per vehicle instead of one per free
+//     step, without the per-step divergent arrival branch;
+//  2. the dense timeline, step by step, from the vehicle list kept in LDS.
 __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
                                                              int i4, int i10, int i1) {
-    const int64_t e = (int64_t)blockIdx.x * kGenBlock + threadIdx.x;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    uint32_t *s_veh = reinterpret_cast<uint32_t *>(lds);                        // [V][BLOCK] arr | dep<<8 | cap<<16
+    double *s_soc = reinterpret_cast<double *>(s_veh + kDayVehicles * kGenBlock);   // [V][BLOCK]
+    double *s_req = s_soc + kDayVehicles * kGenBlock;                             // [V][BLOCK] (req only)
+    const int tid = threadIdx.x;
+    const int64_t e = (int64_t)blockIdx.x * kGenBlock + tid;
     const int c = blockIdx.y;
     if (e >= E) return;
     const uint64_t day = *s.episode;
@@ -878,37 +896,51 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     HashStream rng{stream_key(seed, ge, (uint32_t)c, day), 0u};
     const int T = p.T, n = p.n;
 
-    bool present = false, prev_occ = false;
-    int dep = 0, prev_rem = 0;
-    uint32_t cap = 0;
-    double req = 0.0;
-    for (int t = 0; t < T; ++t) {
-        bool arrived = false;
-        double soc_arr = 0.0;
-        if (!present) {
-            if (rng.next() >= kArrivalThreshold) {
-                arrived = true;
-                present = true;
-                soc_arr = 0.1 + (0.9 - 0.1) * u32_unit(rng.next());       // uniform(0.1, 0.9)
-                // capacity and departure from one draw: cap = floor(y * 105 / 2^32); the low word of
-                // y * 105 (a bijection of y, uniform given cap) drives the departure
-                const uint32_t y = rng.next();
-                cap = p.diff_caps ? (uint32_t)(15 + below(y, 105)) : 40u;   // randint(15, 120)
-                const uint32_t yd = p.diff_caps ? y * 105u : y;
-                const int hi_c = t + i10, hi_d = T + i1;
-                const int high = hi_c < hi_d ? hi_c : hi_d;
-                const int low = t + i4;
-                dep = (low >= high) ? low : low + below(yd, high - low);
-                if (p.req_enabled) {
-                    const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
-                    req = lo + (1.0 - lo) * u32_unit(rng.next());
-                } else {
-                    req = 1.0;
-                }
-            }
+    // phase 1 (charging_station.py:200-279)
+    int tfree = 0, nv = 0;
+    for (int v = 0; v < kDayVehicles; ++v) {
+        if (tfree >= T) break;
+        const float u = ((float)(rng.next() >> 8) + 1.0f) * 0x1.0p-24f;   // (0, 1]
+        const int ta = tfree + (int)(__log2f(u) * kInvLog2Q);             // floor: the product is >= 0
+        if (ta >= T) break;
+        const double soc_arr = 0.1 + (0.9 - 0.1) * u32_unit(rng.next());   // uniform(0.1, 0.9)
+        // capacity and departure from one draw: cap = floor(y * 105 / 2^32); the low word of
+        // y * 105 (a bijection of y, uniform given cap) drives the departure
+        const uint32_t y = rng.next();
+        const uint32_t cap = p.diff_caps ? (uint32_t)(15 + below(y, 105)) : 40u;   // randint(15, 120)
+        const uint32_t yd = p.diff_caps ? y * 105u : y;
+        const int hi_c = ta + i10, hi_d = T + i1;
+        const int high = hi_c < hi_d ? hi_c : hi_d;
+        const int low = ta + i4;
+        const int dep = (low >= high) ? low : low + below(yd, high - low);
+        s_veh[v * kGenBlock + tid] = (uint32_t)ta | ((uint32_t)dep << 8) | (cap << 16);
+        s_soc[v * kGenBlock + tid] = soc_arr;
+        if (p.req_enabled) {
+            const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
+            s_req[v * kGenBlock + tid] = lo + (1.0 - lo) * u32_unit(rng.next());
         }
-        const bool occ = present && t < dep;
-        if (!occ) present = false;
+        nv = v + 1;
+        tfree = dep + 1;   // the departure step stays empty (charging_station.py:247-255)
+    }
+
+    // phase 2: the timeline
+    int v = 0;
+    uint32_t cur = nv > 0 ? s_veh[tid] : 0xffu;   // arrival 255: no vehicle
+    double soc_cur = nv > 0 ? s_soc[tid] : 0.0;
+    double req_cur = (nv > 0 && p.req_enabled) ? s_req[tid] : 1.0;
+    bool prev_occ = false;
+    int prev_rem = 0;
+    for (int t = 0; t < T; ++t) {
+        if (t > (int)((cur >> 8) & 0xffu) && v < nv) {   // past the current departure: next vehicle
+            ++v;
+            cur = v < nv ? s_veh[v * kGenBlock + tid] : 0xffu;
+            soc_cur = v < nv ? s_soc[v * kGenBlock + tid] : 0.0;
+            req_cur = (v < nv && p.req_enabled) ? s_req[v * kGenBlock + tid] : 1.0;
+        }
+        const int ta = (int)(cur & 0xffu), dep = (int)((cur >> 8) & 0xffu);
+        const uint32_t cap = (cur >> 16) & 0xffu;
+        const bool occ = t >= ta && t < dep;
+        const bool arrived = t == ta;
         // penalty-check list built by observe(t-1) (charging_station.py:42-63)
         bool pen = false;
         if (t > 0 && prev_occ) {
@@ -924,8 +956,8 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const size_t row = ((size_t)t * n + c) * (size_t)E;
         const uint32_t el = (uint32_t)e;
         SNG_GST(s.word[row + el], pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem));
-        SNG_GST(s.aux[row + el], arrived ? soc_arr : 0.0);   // dense: full-line stores
-        if (p.req_stream) SNG_GST(s.req[row + el], pen ? req : 0.0);
+        SNG_GST(s.aux[row + el], arrived ? soc_cur : 0.0);   // dense: full-line stores
+        if (p.req_stream) SNG_GST(s.req[row + el], pen ? req_cur : 0.0);
         prev_occ = occ;
         prev_rem = rem;
     }
@@ -1030,7 +1062,8 @@ hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, do
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            hipStream_t stream) {
     const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)p.n), block(kGenBlock);
-    hipLaunchKernelGGL(generate_kernel, grid, block, 0, stream, p, s, seed, E, i4, i10, i1);
+    hipLaunchKernelGGL(generate_kernel, grid, block, generate_lds_bytes(p.req_enabled != 0), stream, p, s, seed, E, i4,
+                       i10, i1);
     return hipGetLastError();
 }
 

@@ -209,6 +209,32 @@ def test_device_rng_day_distribution_and_invariants():
         assert (venv.last_info()["flags"] == 0).all()
     # mean occupancy over the day, reference generator: ~0.71 at N=10
     assert 0.66 < np.mean(occupancy) < 0.76
+    # the occupancy curve over the day and the stay-length distribution at arrival match the
+    # reference process (oracle MT draws, 3,000 days); occupancy reads from the departure column
+    ref_curve, ref_stay = np.zeros(24), np.zeros(12)
+    dev_stay = np.zeros(12)
+    for i in range(3000):
+        e = O.OracleEnv(cfg, 90_000 + i)
+        o = e.reset()
+        prev = np.zeros(N)
+        for t in range(24):
+            o, _, _, _ = e.step(np.zeros(cfg.act_dim, np.float32))
+            d = np.rint(o[8 + N:8 + 2 * N] * 24)
+            ref_curve[t] += (d > 0).mean() / 3000
+            new = (d > 0) & (prev == 0)   # a vehicle that was not there at t-1 (departure steps are empty)
+            for x in d[new]:
+                ref_stay[min(int(x), 11)] += 1
+            prev = d
+    np.testing.assert_allclose(np.array(occupancy), ref_curve, atol=0.02)
+    venv.reset_tensors()
+    prev = torch.zeros((E, N), device=venv.device)
+    for t in range(24):
+        o, r, dn = venv.step_tensors(torch.zeros((E, venv.act_dim), device=venv.device))
+        d = torch.round(o[:, 8 + N:8 + 2 * N] * 24)
+        new = (d > 0) & (prev == 0)
+        dev_stay += torch.bincount(d[new].clamp(max=11).long(), minlength=12).cpu().numpy()[:12]
+        prev = d
+    np.testing.assert_allclose(dev_stay / dev_stay.sum(), ref_stay / ref_stay.sum(), atol=0.01)
     venv.close()
 
 
