@@ -171,7 +171,8 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N, kernel),
                 "kernel": kernel, "bytes_per_launch": bpl,
                 "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src}
-        cpu = None if args.no_cpu_baseline else cpu_baseline(kw, args.cpu_budget)
+        # the CPU baseline is a rank-0, single-GPU report (it would only delay the other ranks' exit)
+        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(kw, args.cpu_budget)
         headline = (N == 10 and T == 24 and not noise)
         metric = METRIC if headline else f"env-steps/sec (whole node) at N={E:,} envs × {N} chargers, {T}-step day"
         desc = f"b-pv bounded sparse {args.time_interval}" + (
