@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing-days", type=int, default=3, help="eager days for the per-kernel HIP-event probe")
+    ap.add_argument("--graph-days", type=int, default=4, help="days per graph replay at N=1 (divides steps)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,7 +129,11 @@ def main():
     acts = acts.contiguous()
     # the bench's info: only the per-env day return (for the all-gather), no diagnostics
     venv._info.flags = None
-    graph = EpisodeGraph(venv, acts, with_reset=True)
+    # days per graph replay: the per-day RCCL gather of day returns needs one day per replay
+    D = 1 if world > 1 else max(1, args.graph_days)
+    while args.steps % D:
+        D -= 1
+    graph = EpisodeGraph(venv, acts, with_reset=True, days=D)
     gathered = torch.empty(world * E, dtype=torch.float64, device=device) if world > 1 else None
 
     def day():
@@ -136,14 +141,14 @@ def main():
         if dist is not None:
             dist.all_gather_into_tensor(gathered, venv.return_d)
 
-    for _ in range(args.warmup):
+    for _ in range(-(-args.warmup // D)):   # at least W warmup days
         day()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(args.steps // D):
         day()
     torch.cuda.synchronize()
     if dist is not None:
@@ -184,6 +189,7 @@ def main():
                                       f"GPU-RNG reset + {T} fused steps per bench step (hipGraph)",
                           "envs_per_gpu": E, "chargers": N, "timesteps": T,
                           "step_unit": "one simulated day of every env",
+                          "days_per_graph_replay": D,
                           "parallelism": f"env-sharded x{world}" + (", RCCL all-gather of day returns" if world > 1 else "")},
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out))

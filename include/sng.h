@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 3
+#define SNG_ABI_VERSION 4
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -212,12 +212,13 @@ int sng_get_vehicle_soc(SngEnv *env, double *host_soc);
 int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_power, double *price,
                    double *price_max, int32_t *n);
 
-/* One full day captured as a hipGraph: [device-RNG reset] + T fused steps.  actions
- * holds T consecutive [num_envs][act_dim] blocks; obs/reward/done are overwritten every
- * step; info may be NULL.  Replays draw a new day each time.  flags: SNG_GRAPH_*. */
-#define SNG_GRAPH_RESET 1   /* start every replay with a device-RNG reset */
+/* `days` full days captured as one hipGraph: ([device-RNG reset] + T fused steps) x days.
+ * actions holds T consecutive [num_envs][act_dim] blocks (reused every day); obs/reward/done
+ * are overwritten every step; info may be NULL.  Replays draw new days each time.
+ * flags: SNG_GRAPH_*; days > 1 needs SNG_GRAPH_RESET. */
+#define SNG_GRAPH_RESET 1   /* start every day with a device-RNG reset */
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
-                     const SngInfo *info, int flags, SngGraph **out);
+                     const SngInfo *info, int flags, int32_t days, SngGraph **out);
 int sng_graph_launch(SngGraph *graph, void *stream);
 /* Kernel-time probe: runs `days` device-RNG days eagerly (as the graph does) and returns the
  * device time (ms) of every step kernel, ms[days*T], from HIP start/stop events attached to

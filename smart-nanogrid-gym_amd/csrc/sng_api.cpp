@@ -880,9 +880,11 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 }
 
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
-                     const SngInfo *info, int flags, SngGraph **out) {
+                     const SngInfo *info, int flags, int32_t days, SngGraph **out) {
     const bool with_reset = (flags & SNG_GRAPH_RESET) != 0;
     if (!env || !actions || !obs || !reward || !done || !out) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    if (days < 1 || (days > 1 && !with_reset))
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "days must be >= 1 (more than one needs SNG_GRAPH_RESET)");
     if (with_reset && !device_rng_ok(env))
         return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
     HIP_TRY(env, hipSetDevice(env->device));
@@ -901,13 +903,15 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
     const int A = p.act_dim;
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
     hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
-    if (e == hipSuccess && with_reset) {
-        e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, cs);
-        if (e == hipSuccess) e = launch_profiles(p, env->ds, E, cs);
-        if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, cs);
+    for (int d = 0; e == hipSuccess && d < days; ++d) {
+        if (with_reset) {
+            e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, cs);
+            if (e == hipSuccess) e = launch_profiles(p, env->ds, E, cs);
+            if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, cs);
+        }
+        for (int t = 0; e == hipSuccess && t < p.T; ++t)
+            e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
     }
-    for (int t = 0; e == hipSuccess && t < p.T; ++t)
-        e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
     hipGraph_t graph = nullptr;
     hipError_t e2 = hipStreamEndCapture(cs, &graph);
     if (e == hipSuccess) e = e2;

@@ -346,21 +346,26 @@ class SmartNanogridVecEnv:
         n = ctypes.c_int32()
         irr = np.zeros(512)
         pv = np.zeros(512)
-        price = np.zeros(48)
+        price = np.zeros(512)   # 48 entries, 2T with the extended day (include/sng.h)
         mx = ctypes.c_double()
         pmx = ctypes.c_double()
         P = _native.c_double_p
         check(lib().sng_get_tables(self._h, irr.ctypes.data_as(P), ctypes.byref(mx), pv.ctypes.data_as(P),
                                    price.ctypes.data_as(P), ctypes.byref(pmx), ctypes.byref(n)), self._h)
-        return dict(irr=irr[:n.value], irr_max=mx.value, pv_power=pv[:n.value], price=price, price_max=pmx.value)
+        n_price = 2 * self.timesteps if self.settings.constants.get("extended_day") else 48
+        return dict(irr=irr[:n.value], irr_max=mx.value, pv_power=pv[:n.value], price=price[:n_price],
+                    price_max=pmx.value)
 
 
 class EpisodeGraph:
-    """A whole day (device-RNG reset + T fused steps) captured once as a hipGraph and
-    replayed; actions come from a device tensor [T, E, act_dim]."""
+    """Whole days (device-RNG reset + T fused steps, x days) captured once as a hipGraph and
+    replayed; actions come from a device tensor [T, E, act_dim] reused every day."""
 
-    def __init__(self, venv, actions, with_reset=True):
+    def __init__(self, venv, actions, with_reset=True, days=1):
+        """days > 1 captures that many consecutive days (each with its reset) in one graph,
+        which amortises the graph launch."""
         self.venv = venv
+        self.days = int(days)
         self.actions = actions.contiguous()
         g = ctypes.c_void_p()
         with torch.cuda.device(venv.device):
@@ -368,7 +373,7 @@ class EpisodeGraph:
                                          ctypes.c_void_p(venv.obs_d.data_ptr()),
                                          ctypes.c_void_p(venv.reward_d.data_ptr()),
                                          ctypes.c_void_p(venv.done_d.data_ptr()), ctypes.byref(venv._info),
-                                         int(with_reset), ctypes.byref(g)), venv._h)
+                                         int(with_reset), self.days, ctypes.byref(g)), venv._h)
         self._g = g
 
     def launch(self, stream=None):
