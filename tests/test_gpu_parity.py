@@ -395,3 +395,27 @@ def test_unaligned_actions_take_the_scalar_staging_path(E, N):
         assert torch.equal(oa, ob) and torch.equal(ra, rb) and torch.equal(da, db)
     a.close()
     b.close()
+
+
+def test_multi_day_graph_matches_eager_days():
+    """EpisodeGraph(days=3): three device-RNG days per replay equal three eager days."""
+    E, N = 4096, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    a = SmartNanogridVecEnv(E, seed=5, rng="device", **kw)
+    b = SmartNanogridVecEnv(E, seed=5, rng="device", **kw)
+    graph = EpisodeGraph(b, acts, days=3)
+    for rep in range(2):
+        for day in range(3):
+            a.reset_tensors()
+            for t in range(24):
+                oa, ra, da = a.step_tensors(acts[t])
+        graph.launch()
+        torch.cuda.synchronize()
+        assert torch.equal(oa, b.obs_d) and torch.equal(ra, b.reward_d) and torch.equal(a.return_d, b.return_d)
+        np.testing.assert_array_equal(a.battery_state_of_charge(), b.battery_state_of_charge())
+    graph.close()
+    a.close()
+    b.close()
