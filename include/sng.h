@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 4
+#define SNG_ABI_VERSION 5
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -142,6 +142,9 @@ typedef struct SngInfo {
     double *initial_battery_soc;         /* 'Initial battery state of charge' */
     uint32_t *flags;                     /* SNG_FLAG_* raised by this step */
     double *episode_return;              /* accumulated: += reward (zeroed by every reset) */
+    /* per charger, [num_envs][N] (row-major, env-major); NULL = not written */
+    double *charger_power;               /* 'Charger power values' (charging_station.py:282-299) */
+    double *vehicle_soc;                 /* SOC[c, t] after the step (charger.py:36-53/:86/:133) */
 } SngInfo;
 
 /* A scenario in the reference's own layout (ChargingStation after
@@ -207,6 +210,19 @@ int sng_set_battery_soc(SngEnv *env, const double *host_soc);
 int sng_get_pv_ratio(SngEnv *env, double *host_ratio);
 /* EV state of charge SOC[c, t] after the last step, host [num_envs][N]. */
 int sng_get_vehicle_soc(SngEnv *env, double *host_soc);
+
+/* The current day of env `env_index` in the reference's initial_values.json layout
+ * (ChargingStation.generated_initial_values_json, charging_station.py:164-191), decoded from
+ * the device timeline -- for host-generated, device-generated and injected days alike.
+ * soc / occupancy / capacity / requested_soc: host [N][slots]; arrivals / departures: host
+ * [N][max_vehicles], -1 padded (n_vehicles[N] holds the full counts); pv_ratio: one double.
+ * 'SOC' holds the arrival SoCs and the recorded SOC[c, t] of empty chargers (the slots a step
+ * reads); Requested_SOC is exact when requested SoC is enabled or any penalised value differs
+ * from 1.0, and 1.0 on occupied slots otherwise.  Valid after a reset until the next reset;
+ * synchronises the device. */
+int sng_get_scenario(SngEnv *env, int64_t env_index, int32_t max_vehicles, double *soc, double *occupancy,
+                     double *capacity, double *requested_soc, int32_t *arrivals, int32_t *departures,
+                     int32_t *n_vehicles, double *pv_ratio);
 
 /* Constant tables as built at create (host copies; n = 2*T). */
 int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_power, double *price,

@@ -292,13 +292,9 @@ bool encode_day(const Params &p, int64_t E, int64_t e, const DayView &d, uint32_
             const size_t idx = ((size_t)t * N + c) * (size_t)E + (size_t)e;
             word[idx] = pack_word(occupied, !running, pen, capv, rem);
             aux[idx] = a;
-            if (pen) {
-                const double rq = req[t - 1];
-                if (rq != 1.0) *need_req = true;
-                if (req_out) req_out[idx] = rq;
-            } else if (req_out) {
-                req_out[idx] = 0.0;
-            }
+            if (pen && req[t - 1] != 1.0) *need_req = true;
+            // Requested_SOC[c, t-1]; slot 0 keeps Requested_SOC[c, T-1] (sng_layout.h)
+            if (req_out) req_out[idx] = req[t >= 1 ? t - 1 : T - 1];
         }
         // penalty at t = 0 reads python index -1 (slot 24) of SOC / Requested_SOC (penaliser.py:59-69)
         if (occ[0] != 0.0 && penalty_window(p.penalty_mode, dep, nd, 0)) {
@@ -405,6 +401,8 @@ InfoPtrs info_ptrs(const SngInfo *i) {
     o.bess_initial = i->initial_battery_soc;
     o.flags = i->flags;
     o.episode_return = i->episode_return;
+    o.charger_power = i->charger_power;
+    o.vehicle_soc = i->vehicle_soc;
     return o;
 }
 
@@ -863,6 +861,72 @@ int sng_get_vehicle_soc(SngEnv *env, double *h) {
     HIP_TRY(env, hipMemcpy(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost));
     for (int64_t e = 0; e < env->E; ++e)
         for (int c = 0; c < N; ++c) h[e * N + c] = tmp[(size_t)c * env->E + e];
+    return SNG_OK;
+}
+
+// Inverse of encode_day / generate_kernel for one env: the word stream gives occupancy,
+// capacity and (at each arrival, W_STATIC on an occupied step) the departure; aux gives the
+// arrival SoC and the SOC[c, t] of empty chargers; the req stream holds Requested_SOC[c, t-1]
+// at t >= 1 and Requested_SOC[c, T-1] at t = 0.
+int sng_get_scenario(SngEnv *env, int64_t e, int32_t V, double *soc, double *occupancy, double *capacity,
+                     double *requested_soc, int32_t *arrivals, int32_t *departures, int32_t *n_vehicles,
+                     double *pv_ratio) {
+    if (!env || !soc || !occupancy || !capacity || !requested_soc || !arrivals || !departures || !n_vehicles ||
+        !pv_ratio)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    if (e < 0 || e >= env->E || V < 1) return fail(env, SNG_ERR_INVALID_ARGUMENT, "env_index or max_vehicles out of range");
+    if (env->t < 0) return fail(env, SNG_ERR_STATE, "no day yet: call reset()");
+    HIP_TRY(env, hipSetDevice(env->device));
+    HIP_TRY(env, hipDeviceSynchronize());
+    const int N = env->p.n, T = env->p.T, S = env->slots;
+    const size_t rows = (size_t)T * N, pitch = (size_t)env->E;
+    std::vector<uint32_t> w(rows);
+    std::vector<double> aux(rows), rq;
+    HIP_TRY(env, hipMemcpy2D(w.data(), sizeof(uint32_t), env->ds.word + e, pitch * sizeof(uint32_t), sizeof(uint32_t),
+                             rows, hipMemcpyDeviceToHost));
+    HIP_TRY(env, hipMemcpy2D(aux.data(), sizeof(double), env->ds.aux + e, pitch * sizeof(double), sizeof(double), rows,
+                             hipMemcpyDeviceToHost));
+    const bool have_req = env->p.req_stream && env->ds.req;
+    if (have_req) {
+        rq.resize(rows);
+        HIP_TRY(env, hipMemcpy2D(rq.data(), sizeof(double), env->ds.req + e, pitch * sizeof(double), sizeof(double),
+                                 rows, hipMemcpyDeviceToHost));
+    }
+    HIP_TRY(env, hipMemcpy(pv_ratio, env->ds.ratio + e, sizeof(double), hipMemcpyDeviceToHost));
+    std::fill(soc, soc + (size_t)N * S, 0.0);
+    std::fill(occupancy, occupancy + (size_t)N * S, 0.0);
+    std::fill(capacity, capacity + (size_t)N * S, 0.0);
+    std::fill(requested_soc, requested_soc + (size_t)N * S, 0.0);
+    std::fill(arrivals, arrivals + (size_t)N * V, -1);
+    std::fill(departures, departures + (size_t)N * V, -1);
+    for (int c = 0; c < N; ++c) {
+        int nv = 0;
+        for (int t = 0; t < T; ++t) {
+            const size_t i = (size_t)t * N + c;
+            const uint32_t word = w[i];
+            const bool occ = (word & W_OCC) != 0;
+            const size_t o = (size_t)c * S + t;
+            if (occ) {
+                occupancy[o] = 1.0;
+                capacity[o] = (double)((word >> W_CAP_SHIFT) & 0xffu);
+                if (word & W_STATIC) {   // arrival: SOC[c, t] as generated, departure t + remaining
+                    soc[o] = aux[i];
+                    if (nv < V) {
+                        arrivals[(size_t)c * V + nv] = t;
+                        departures[(size_t)c * V + nv] = t + (int)((word >> W_DEP_SHIFT) & 0xffu);
+                    }
+                    ++nv;
+                }
+            } else {
+                soc[o] = aux[i];
+            }
+            if (have_req)
+                requested_soc[o] = rq[(t + 1 < T ? (size_t)(t + 1) * N : 0) + c];
+            else
+                requested_soc[o] = occ ? 1.0 : 0.0;
+        }
+        n_vehicles[c] = nv;
+    }
     return SNG_OK;
 }
 

@@ -689,6 +689,10 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                 if (c >= cend) break;
                 const ChargerResult r = charger_step<FAST>(p, w[j], aux[j], run[j], req[j], av[j], t, rc[j]);
                 SNG_ST(socv[(size_t)c * E + e], r.soc);
+                if (DIAG) {   // 'Charger power values' and the SOC[c, t] the day record holds
+                    if (info.charger_power) info.charger_power[(size_t)e * n + c] = r.pw;
+                    if (info.vehicle_soc) info.vehicle_soc[(size_t)e * n + c] = r.soc;
+                }
                 o_row[k_soc + c] = (float)r.soc;
                 o_row[k_soc + n + c] = departure_obs(w[j]);
                 n_nonexist += r.nx;
@@ -957,10 +961,13 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const uint32_t el = (uint32_t)e;
         SNG_GST(s.word[row + el], pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem));
         SNG_GST(s.aux[row + el], arrived ? soc_cur : 0.0);   // dense: full-line stores
-        if (p.req_stream) SNG_GST(s.req[row + el], pen ? req_cur : 0.0);
+        // requested SoC timeline (sng_layout.h): Requested_SOC[c, t-1] at t >= 1 -- the step reads
+        // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
+        if (p.req_stream && t > 0) SNG_GST(s.req[row + el], prev_occ ? req_cur : 0.0);
         prev_occ = occ;
         prev_rem = rem;
     }
+    if (p.req_stream) SNG_GST(s.req[(size_t)c * E + (uint32_t)e], prev_occ ? req_cur : 0.0);
     if (c == 0) {
         HashStream r2{stream_key(seed, ge, 0x7a710000u, day), 0u};            // the PV-ratio domain
         s.ratio[e] = (double)below(r2.next(), 181) / 100;   // random.randint(0, 180) / 100
@@ -1037,7 +1044,8 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
     const LaunchEvents *ev = (ev_start && ev_stop) ? &evs : nullptr;
     const bool diag = info.grid_power || info.p_charge || info.p_discharge || info.bess_soc || info.pen_vehicle ||
                       info.pen_battery || info.grid_cost || info.total_cost || info.solar || info.bess_power ||
-                      info.bess_calc_power || info.nonexistent || info.bess_initial;
+                      info.bess_calc_power || info.nonexistent || info.bess_initial || info.charger_power ||
+                      info.vehicle_soc;
     if (diag)
         launch_step_n<true>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev);
     else

@@ -12,7 +12,9 @@
 //   aux    f64 [T][N][E]    per charger-step static SoC: the "previous" SoC when the word's
 //                           STATIC bit is set (arrival: SOC[c, t] as generated), else the
 //                           SOC[c, t] an unoccupied charger shows
-//   req    f64 [T][N][E]    requested SoC of the vehicle at t-1 (penalty), only when enabled
+//   req    f64 [T][N][E]    Requested_SOC[c, t-1] (read by the penalty check where W_PEN is set);
+//                           the t = 0 slot, never read by a step, holds Requested_SOC[c, T-1] so the
+//                           day can be exported (sng_get_scenario); only when enabled
 //   flags  u32 [E]          sticky SNG_FLAG_* bits
 //
 // word bits (one u32 per charger and timestep):
@@ -98,6 +100,7 @@ struct InfoPtrs {
         *solar, *bess_power, *bess_calc_power, *nonexistent, *bess_initial;
     uint32_t *flags;
     double *episode_return;
+    double *charger_power, *vehicle_soc;   // [E][N], DIAG only
 };
 
 }  // namespace sng

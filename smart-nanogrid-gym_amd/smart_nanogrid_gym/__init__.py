@@ -6,10 +6,12 @@
 with the reference's id and max_episode_steps (smart_nanogrid_gym/__init__.py:4-8).
 """
 from .envs import SmartNanogridEnv
+from .recorder import DayRecorder
 from .settings import EnvSettings, parse_time_interval
 from .vec_env import EpisodeGraph, SmartNanogridVecEnv
 
-__all__ = ["SmartNanogridEnv", "SmartNanogridVecEnv", "EpisodeGraph", "EnvSettings", "parse_time_interval"]
+__all__ = ["SmartNanogridEnv", "SmartNanogridVecEnv", "EpisodeGraph", "EnvSettings", "DayRecorder",
+           "parse_time_interval"]
 
 
 def _register():

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SNG_LIBRARY", os.path.join(os.path.dirname(PKG_DIR), 
 DATA_DIR = os.path.join(PKG_DIR, "data")
 IRRADIANCE_FILE = os.path.join(DATA_DIR, "solar_irradiance_1min.f64")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 SNG_OK = 0
 RNG_REFERENCE = 0
 RNG_DEVICE = 1
@@ -83,7 +83,9 @@ INFO_FIELDS = ["grid_power", "total_charging_power", "total_discharging_power", 
 
 class SngInfo(ctypes.Structure):
     _fields_ = [(f, ctypes.c_void_p) for f in INFO_FIELDS] + [("flags", ctypes.c_void_p),
-                                                               ("episode_return", ctypes.c_void_p)]
+                                                               ("episode_return", ctypes.c_void_p),
+                                                               ("charger_power", ctypes.c_void_p),
+                                                               ("vehicle_soc", ctypes.c_void_p)]
 
 
 class SngScenario(ctypes.Structure):
@@ -113,6 +115,8 @@ EXPORTS = {
     "sng_set_battery_soc": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "sng_get_pv_ratio": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
     "sng_get_vehicle_soc": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
+    "sng_get_scenario": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, c_double_p, c_double_p,
+                                        c_double_p, c_double_p, c_int32_p, c_int32_p, c_int32_p, c_double_p]),
     "sng_get_tables": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
                                       c_int32_p]),
     "sng_graph_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

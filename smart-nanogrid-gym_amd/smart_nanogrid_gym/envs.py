@@ -8,6 +8,7 @@ Same constructor keywords, same spaces, reset() -> (obs, {}), step(a) ->
 import numpy as np
 import torch
 
+from .recorder import DayRecorder
 from .vec_env import SmartNanogridVecEnv
 
 try:  # subclass gym(nasium).Env when available so wrappers / checkers accept it
@@ -28,7 +29,10 @@ class SmartNanogridEnv(_Base):
                  battery_system_available_in_model=True, vehicle_to_everything=False,
                  enable_different_vehicle_battery_capacities=True, enable_requested_state_of_charge=False,
                  algorithm_used="", environment_mode="", time_interval="", charging_mode="",
-                 vehicle_uncharged_penalty_mode="", *, seed=0, device=0, rng="reference", **extra):
+                 vehicle_uncharged_penalty_mode="", *, seed=0, device=0, rng="reference", results_directory=None,
+                 **extra):
+        """results_directory: write the reference's per-day prediction_results / initial_values
+        files there (smart_nanogrid_environment.py:239-309; DayRecorder); None = no files."""
         self._venv = SmartNanogridVecEnv(
             1, seed=seed, device=device, rng=rng, price_model=price_model, number_of_chargers=number_of_chargers,
             pv_system_available_in_model=pv_system_available_in_model,
@@ -44,6 +48,7 @@ class SmartNanogridEnv(_Base):
         self.TIME_INTERVAL = self._venv.settings.time_interval
         self.simulated_single_day = False
         self.timestep = None
+        self.recorder = DayRecorder(self._venv, [0], results_directory) if results_directory is not None else None
 
     def reset(self, generate_new_initial_values=True, algorithm_used="", environment_mode="", **kwargs):
         """smart_nanogrid_environment.py:320-360 (gym-0.26 `seed=`/`options=` are accepted and ignored,

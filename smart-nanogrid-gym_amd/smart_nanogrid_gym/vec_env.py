@@ -78,13 +78,13 @@ class SmartNanogridVecEnv:
         self.flags_d = torch.zeros(E, dtype=torch.int32, device=dev)
         self.return_d = torch.zeros(E, dtype=torch.float64, device=dev)
         self.info_d = {}
-        if info:
-            self.info_d = {f: torch.zeros(E, dtype=torch.float64, device=dev) for f in _native.INFO_FIELDS}
+        self.charger_power_d = self.vehicle_soc_d = None
+        self._recorders = []
         self._info = _native.SngInfo()
-        for f, t in self.info_d.items():
-            setattr(self._info, f, t.data_ptr())
         self._info.flags = self.flags_d.data_ptr()
         self._info.episode_return = self.return_d.data_ptr()
+        if info:
+            self._enable_info()
         # pinned host mirrors for the numpy (SB3) path
         pin = dict(pin_memory=True)
         self._act_h = torch.zeros((E, self.act_dim), dtype=torch.float32, **pin)
@@ -110,6 +110,28 @@ class SmartNanogridVecEnv:
         except Exception:
             pass
 
+    def _enable_info(self, per_charger=False):
+        """Allocate the SngInfo diagnostics (and, per_charger, the [E, N] power / SoC arrays the
+        day recorder reads); the step kernel writes them from then on."""
+        E, N, dev = self.num_envs, self.settings.number_of_chargers, self.device
+        if not self.info_d:
+            self.info_d = {f: torch.zeros(E, dtype=torch.float64, device=dev) for f in _native.INFO_FIELDS}
+            for f, t in self.info_d.items():
+                setattr(self._info, f, t.data_ptr())
+        if per_charger and self.charger_power_d is None:
+            self.charger_power_d = torch.zeros((E, N), dtype=torch.float64, device=dev)
+            self.vehicle_soc_d = torch.zeros((E, N), dtype=torch.float64, device=dev)
+            self._info.charger_power = self.charger_power_d.data_ptr()
+            self._info.vehicle_soc = self.vehicle_soc_d.data_ptr()
+
+    def attach_recorder(self, recorder):
+        """Called by DayRecorder: notified after every reset and step of this env batch."""
+        self._enable_info(per_charger=True)
+        self._recorders.append(recorder)
+
+    def detach_recorder(self, recorder):
+        self._recorders = [r for r in self._recorders if r is not recorder]
+
     @property
     def timestep(self):
         return lib().sng_get_timestep(self._h)
@@ -127,6 +149,8 @@ class SmartNanogridVecEnv:
             self.return_d.zero_()
             check(lib().sng_reset(self._h, mode, ctypes.c_void_p(self.obs_d.data_ptr()),
                                   _stream_handle(self.device)), self._h)
+        for r in self._recorders:
+            r.day_started()
         return self.obs_d
 
     def step_tensors(self, actions):
@@ -140,6 +164,8 @@ class SmartNanogridVecEnv:
             check(lib().sng_step(self._h, ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(self.obs_d.data_ptr()),
                                  ctypes.c_void_p(self.reward_d.data_ptr()), ctypes.c_void_p(self.done_d.data_ptr()),
                                  ctypes.byref(self._info), _stream_handle(self.device)), self._h)
+        for r in self._recorders:
+            r.step_done(actions)
         return self.obs_d, self.reward_d, self.done_d
 
     def reset_from_initial_values(self, initial_values, pv_ratio, restore_requested_soc=False):
@@ -197,6 +223,8 @@ class SmartNanogridVecEnv:
             check(lib().sng_reset_from_scenario(self._h, ctypes.byref(sc), ctypes.c_void_p(self.obs_d.data_ptr()),
                                                 _stream_handle(self.device)), self._h)
             torch.cuda.current_stream(self.device).synchronize()
+        for r in self._recorders:
+            r.day_started()
         return self._obs_to_host()
 
     # ------------------------------------------------------------------ SB3 VecEnv API
@@ -328,6 +356,28 @@ class SmartNanogridVecEnv:
         out = np.zeros((self.num_envs, self.settings.number_of_chargers))
         check(lib().sng_get_vehicle_soc(self._h, out.ctypes.data_as(_native.c_double_p)), self._h)
         return out
+
+    def get_scenario(self, env_index=0, max_vehicles=32):
+        """The current day of env `env_index` as the reference's initial_values.json dict
+        (ChargingStation.generated_initial_values_json, charging_station.py:164-191) and its PV
+        ratio, decoded from the device timeline (sng_get_scenario in include/sng.h)."""
+        N, S, V = self.settings.number_of_chargers, self.slots, int(max_vehicles)
+        f = [np.zeros((N, S)) for _ in range(4)]
+        arr = np.full((N, V), -1, np.int32)
+        dep = np.full((N, V), -1, np.int32)
+        nv = np.zeros(N, np.int32)
+        ratio = ctypes.c_double()
+        P, I = _native.c_double_p, _native.c_int32_p
+        check(lib().sng_get_scenario(self._h, int(env_index), V, *[a.ctypes.data_as(P) for a in f],
+                                     arr.ctypes.data_as(I), dep.ctypes.data_as(I), nv.ctypes.data_as(I),
+                                     ctypes.byref(ratio)), self._h)
+        if (nv > V).any():
+            return self.get_scenario(env_index, int(nv.max()))
+        soc, occ, cap, req = f
+        iv = {"SOC": soc.tolist(), "Arrivals": [arr[c, :nv[c]].tolist() for c in range(N)],
+              "Departures": [dep[c, :nv[c]].tolist() for c in range(N)], "Charger_occupancy": occ.tolist(),
+              "Vehicle_capacities": cap.tolist(), "Requested_SOC": req.tolist()}
+        return iv, ratio.value
 
     def time_step_kernels(self, actions, days=1):
         """Device time (ms) of every step kernel over `days` eager device-RNG days, from HIP

@@ -22,6 +22,7 @@ STEPS="${STEPS:-tests smoke bench prof}"
 for s in $STEPS; do
   case $s in
     tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} ;;
+    one)   run pytest_one 600 python -m pytest ${ONE_TESTS:-tests/test_gpu_recorder.py} -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     sweep) for l in 1 2 4; do run bench_l$l 300 python bench.py --no-cpu-baseline --lanes $l; done ;;
