@@ -25,6 +25,7 @@ for s in $STEPS; do
     one)   run pytest_one 600 python -m pytest ${ONE_TESTS:-tests/test_gpu_recorder.py} -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    ab)    for a in ${AB_ARGS:-"--pipeline 0" "--pipeline 1"}; do run "bench_ab_${a// /_}" 300 python bench.py --no-cpu-baseline $a; done ;;
     sweep) for l in 1 2 4; do run bench_l$l 300 python bench.py --no-cpu-baseline --lanes $l; done ;;
     sq)    for l in ${SQ_LANES:-1 2}; do run sq_l$l 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/sq_l$l -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 --lanes $l; done ;;
     stamps) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so run stamps 300 python tools/stamps.py 1 2 4 ;;
