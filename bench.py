@@ -2,9 +2,10 @@
 
 Metric (BASELINE.json): env-steps/sec (whole node) at 65,536 envs x 10 chargers, 24-step day.
 One bench "step" = one simulated day for every env on every GPU: GPU-RNG reset (new
-vehicles) + 24 fused step kernels (+ one RCCL all-gather of the per-env day returns when
-N > 1), replayed as one hipGraph.  Actions are synthetic (uniform in the action Box, 20 %
-exact zeros), pre-generated on the device outside the timed region.
+vehicles) + 24 fused step kernels, replayed as hipGraphs of 4 days.  When N > 1 every day's
+per-env returns are all-gathered over RCCL, one collective per replay on the collective
+stream, overlapped with the next replay's kernels.  Actions are synthetic (uniform in the
+action Box, 20 % exact zeros), pre-generated on the device outside the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--chargers C] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -93,7 +94,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing-days", type=int, default=3, help="eager days for the per-kernel HIP-event probe")
-    ap.add_argument("--graph-days", type=int, default=4, help="days per graph replay at N=1 (divides steps)")
+    ap.add_argument("--graph-days", type=int, default=4, help="days per graph replay (divides steps)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -108,7 +109,7 @@ def main():
     torch.cuda.set_device(device)
 
     from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv
-    from smart_nanogrid_gym.parallel import max_over_ranks, shard_envs
+    from smart_nanogrid_gym.parallel import DayReturnExchange, max_over_ranks, shard_envs
 
     E, N = args.envs, args.chargers
     kw = dict(number_of_chargers=N, time_interval=args.time_interval, charging_mode="bounded",
@@ -129,20 +130,34 @@ def main():
     acts = acts.contiguous()
     # the bench's info: only the per-env day return (for the all-gather), no diagnostics
     venv._info.flags = None
-    # days per graph replay: the per-day RCCL gather of day returns needs one day per replay
-    D = 1 if world > 1 else max(1, args.graph_days)
+    # days per graph replay (the same at every N, so per-GPU work is identical)
+    D = max(1, args.graph_days)
     while args.steps % D:
         D -= 1
-    graph = EpisodeGraph(venv, acts, with_reset=True, days=D)
-    gathered = torch.empty(world * E, dtype=torch.float64, device=device) if world > 1 else None
+    xch = None
+    if dist is not None:
+        # N > 1: every day's per-env returns land in a [D, E] snapshot (one per graph, two
+        # alternating graphs) and one RCCL all-gather per replay runs on the collective stream
+        # while the next replay computes
+        xch = DayReturnExchange(D, E, device)
+        graphs = [EpisodeGraph(venv, acts, with_reset=True, days=D, day_returns=xch.snap[k]) for k in range(2)]
+    else:
+        graphs = [EpisodeGraph(venv, acts, with_reset=True, days=D)]
+    rep = [0]
 
-    def day():
-        graph.launch()
-        if dist is not None:
-            dist.all_gather_into_tensor(gathered, venv.return_d)
+    def day():   # one graph replay = D simulated days
+        k = rep[0] % len(graphs)
+        if xch is not None:
+            xch.acquire(k)
+        graphs[k].launch()
+        if xch is not None:
+            xch.gather(k)
+        rep[0] += 1
 
     for _ in range(-(-args.warmup // D)):   # at least W warmup days
         day()
+    if xch is not None:
+        xch.finish()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -150,6 +165,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps // D):
         day()
+    if xch is not None:
+        xch.finish()   # the last replay's gather is part of the timed work
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -164,6 +181,10 @@ def main():
     # sanity: a day's returns are finite and <= 0
     ret = venv.return_d.cpu().numpy()
     assert np.isfinite(ret).all() and (ret <= 0).all()
+    if xch is not None:   # every rank's returns of every day of the last replays arrived
+        for k in range(2):
+            got = xch.gathered(k).cpu().numpy()
+            assert got.shape == (D, world * E) and np.isfinite(got).all() and (got <= 0).all() and (got < 0).any()
 
     if rank == 0:
         env_steps = world * E * T * args.steps
@@ -190,10 +211,12 @@ def main():
                           "envs_per_gpu": E, "chargers": N, "timesteps": T,
                           "step_unit": "one simulated day of every env",
                           "days_per_graph_replay": D,
-                          "parallelism": f"env-sharded x{world}" + (", RCCL all-gather of day returns" if world > 1 else "")},
+                          "parallelism": f"env-sharded x{world}" + (
+                              ", RCCL all-gather of every day's returns, one per replay, overlapped" if world > 1 else "")},
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out))
-    graph.close()
+    for gr in graphs:
+        gr.close()
     venv.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 5
+#define SNG_ABI_VERSION 6
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -231,10 +231,13 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 /* `days` full days captured as one hipGraph: ([device-RNG reset] + T fused steps) x days.
  * actions holds T consecutive [num_envs][act_dim] blocks (reused every day); obs/reward/done
  * are overwritten every step; info may be NULL.  Replays draw new days each time.
- * flags: SNG_GRAPH_*; days > 1 needs SNG_GRAPH_RESET. */
+ * flags: SNG_GRAPH_*; days > 1 needs SNG_GRAPH_RESET.
+ * day_returns (device [days][num_envs] f64, may be NULL): day d's returns accumulate into row
+ * d instead of info->episode_return, so a replay leaves every day's returns for one
+ * collective per replay (bench.py gathers them over RCCL while the next replay runs). */
 #define SNG_GRAPH_RESET 1   /* start every day with a device-RNG reset */
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
-                     const SngInfo *info, int flags, int32_t days, SngGraph **out);
+                     const SngInfo *info, int flags, int32_t days, double *day_returns, SngGraph **out);
 int sng_graph_launch(SngGraph *graph, void *stream);
 /* Kernel-time probe: runs `days` device-RNG days eagerly (as the graph does) and returns the
  * device time (ms) of every step kernel, ms[days*T], from HIP start/stop events attached to

@@ -944,7 +944,7 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 }
 
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
-                     const SngInfo *info, int flags, int32_t days, SngGraph **out) {
+                     const SngInfo *info, int flags, int32_t days, double *day_returns, SngGraph **out) {
     const bool with_reset = (flags & SNG_GRAPH_RESET) != 0;
     if (!env || !actions || !obs || !reward || !done || !out) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     if (days < 1 || (days > 1 && !with_reset))
@@ -968,13 +968,15 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
     hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal);
     for (int d = 0; e == hipSuccess && d < days; ++d) {
+        InfoPtrs ipd = ip;   // day d's returns into row d (observe0 zeroes it, every step adds)
+        if (day_returns) ipd.episode_return = day_returns + (size_t)d * E;
         if (with_reset) {
             e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, cs);
             if (e == hipSuccess) e = launch_profiles(p, env->ds, E, cs);
-            if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, cs);
+            if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ipd.episode_return, E, vec, cs);
         }
         for (int t = 0; e == hipSuccess && t < p.T; ++t)
-            e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
+            e = launch_step(p, env->ds, ipd, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
     }
     hipGraph_t graph = nullptr;
     hipError_t e2 = hipStreamEndCapture(cs, &graph);

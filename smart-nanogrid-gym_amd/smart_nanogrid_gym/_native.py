@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SNG_LIBRARY", os.path.join(os.path.dirname(PKG_DIR), 
 DATA_DIR = os.path.join(PKG_DIR, "data")
 IRRADIANCE_FILE = os.path.join(DATA_DIR, "solar_irradiance_1min.f64")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 SNG_OK = 0
 RNG_REFERENCE = 0
 RNG_DEVICE = 1
@@ -121,7 +121,7 @@ EXPORTS = {
                                       c_int32_p]),
     "sng_graph_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.POINTER(SngInfo), ctypes.c_int, ctypes.c_int32,
-                                        ctypes.POINTER(ctypes.c_void_p)]),
+                                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
     "sng_graph_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     "sng_graph_destroy": (None, [ctypes.c_void_p]),
     "sng_time_step_kernels": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

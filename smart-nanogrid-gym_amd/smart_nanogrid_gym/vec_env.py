@@ -411,19 +411,27 @@ class EpisodeGraph:
     """Whole days (device-RNG reset + T fused steps, x days) captured once as a hipGraph and
     replayed; actions come from a device tensor [T, E, act_dim] reused every day."""
 
-    def __init__(self, venv, actions, with_reset=True, days=1):
+    def __init__(self, venv, actions, with_reset=True, days=1, day_returns=None):
         """days > 1 captures that many consecutive days (each with its reset) in one graph,
-        which amortises the graph launch."""
+        which amortises the graph launch.  day_returns: optional device tensor [days, E] f64;
+        day d's returns accumulate into row d (instead of venv.return_d)."""
         self.venv = venv
         self.days = int(days)
         self.actions = actions.contiguous()
+        self.day_returns = day_returns
+        dr = None
+        if day_returns is not None:
+            if (tuple(day_returns.shape) != (self.days, venv.num_envs) or day_returns.dtype != torch.float64
+                    or day_returns.device != venv.device or not day_returns.is_contiguous()):
+                raise ValueError("day_returns must be a contiguous float64 device tensor [days, num_envs]")
+            dr = ctypes.c_void_p(day_returns.data_ptr())
         g = ctypes.c_void_p()
         with torch.cuda.device(venv.device):
             check(lib().sng_graph_create(venv._h, ctypes.c_void_p(self.actions.data_ptr()),
                                          ctypes.c_void_p(venv.obs_d.data_ptr()),
                                          ctypes.c_void_p(venv.reward_d.data_ptr()),
                                          ctypes.c_void_p(venv.done_d.data_ptr()), ctypes.byref(venv._info),
-                                         int(with_reset), self.days, ctypes.byref(g)), venv._h)
+                                         int(with_reset), self.days, dr, ctypes.byref(g)), venv._h)
         self._g = g
 
     def launch(self, stream=None):

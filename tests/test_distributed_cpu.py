@@ -81,3 +81,46 @@ def test_gloo_world2_gather_matches_single_process():
     np.testing.assert_array_equal(gathered, day_returns(range(TOTAL)))
     assert slowest == 2.0
     assert summary["envs"] == TOTAL and summary["max_return"] <= 0
+
+
+def _xch_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from smart_nanogrid_gym.parallel import DayReturnExchange
+    days, envs = 3, 5
+    x = DayReturnExchange(days, envs, torch.device("cpu"))
+    results = []
+    for rep in range(4):   # alternate buffers; each replay fills days x envs with rank/rep-tagged values
+        k = rep % 2
+        buf = x.acquire(k)
+        buf.copy_(torch.arange(days * envs, dtype=torch.float64).reshape(days, envs) + 1000 * rank + 100 * rep)
+        x.gather(k)
+        if rep >= 1:   # the previous replay's gather, read after its buffer is reacquired
+            x.acquire(1 - k)
+            results.append(x.gathered(1 - k).clone())
+    x.finish()
+    results.append(x.gathered(1).clone())
+    if rank == 0:
+        q.put([r.numpy() for r in results])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_overlapped_day_return_exchange():
+    """DayReturnExchange: double-buffered asynchronous all-gather of [days, E] day returns."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_xch_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    results = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert len(results) == 4
+    base = np.arange(15, dtype=np.float64).reshape(3, 5)
+    for rep, got in enumerate(results):
+        want = np.concatenate([base + 1000 * r + 100 * rep for r in range(2)], axis=1)
+        np.testing.assert_array_equal(got, want)

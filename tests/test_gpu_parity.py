@@ -419,3 +419,52 @@ def test_multi_day_graph_matches_eager_days():
     graph.close()
     a.close()
     b.close()
+
+
+def test_graph_day_returns_and_overlapped_exchange():
+    """EpisodeGraph(day_returns=[D, E]) rows = the eager days' returns; the bench's double-buffered
+    asynchronous RCCL exchange (world 1 here) delivers them while the next replay runs."""
+    import socket
+
+    import torch.distributed as dist
+
+    from smart_nanogrid_gym.parallel import DayReturnExchange
+    E, N, D = 2048, 10, 4
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    a = SmartNanogridVecEnv(E, seed=21, rng="device", **kw)
+    b = SmartNanogridVecEnv(E, seed=21, rng="device", **kw)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        x = DayReturnExchange(D, E, torch.device("cuda", 0))
+        graphs = [EpisodeGraph(b, acts, days=D, day_returns=x.snap[k]) for k in range(2)]
+        want = []
+        for rep in range(4):
+            k = rep % 2
+            x.acquire(k)
+            graphs[k].launch()
+            x.gather(k)
+            days = []
+            for _ in range(D):
+                a.reset_tensors()
+                for t in range(24):
+                    a.step_tensors(acts[t])
+                days.append(a.return_d.clone())
+            want.append(torch.stack(days))
+        x.finish()
+        torch.cuda.synchronize()
+        for k in range(2):   # the last two replays
+            assert torch.equal(x.gathered(k), want[2 + k]), k
+        for gr in graphs:
+            gr.close()
+    finally:
+        dist.destroy_process_group()
+    a.close()
+    b.close()

@@ -25,6 +25,8 @@ for s in $STEPS; do
     one)   run pytest_one 600 python -m pytest ${ONE_TESTS:-tests/test_gpu_recorder.py} -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
+    ablib) i=0; for l in ${AB_LIBS:-libsng_old libsng libsng_old libsng libsng_old libsng}; do i=$((i+1)); SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "ab${i}_$l" 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-}; done
+           for f in $OUT/ab*_*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f) $(grep -o '"mean_launch_us": [0-9.]*' $f)"; done | tee -a $OUT/session.log ;;
     ab)    for a in ${AB_ARGS:-"--pipeline 0" "--pipeline 1"}; do run "bench_ab_${a// /_}" 300 python bench.py --no-cpu-baseline $a; done ;;
     sweep) for l in 1 2 4; do run bench_l$l 300 python bench.py --no-cpu-baseline --lanes $l; done ;;
     sq)    for l in ${SQ_LANES:-1 2}; do run sq_l$l 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/sq_l$l -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 --lanes $l; done ;;
