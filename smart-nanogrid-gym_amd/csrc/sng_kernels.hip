@@ -331,7 +331,7 @@ struct ChargerResult {
 // (validated when a scenario is encoded).
 // FAST (NumPy-2 promotion and dt a power of two, e.g. the 1 h default) is straight-line code, so the
 // compiler interleaves the chargers of an env.
-template <bool FAST>
+template <bool FAST, bool RCP>
 __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, double req,
                                                       float a, int t, double rcap) {
     ChargerResult o;
@@ -364,7 +364,9 @@ __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t 
         const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
         const float pdt = __fmul_rn(pf, p.dt_f);
         pc = (double)pf;
-        change = div_by_cap((double)pdt, cap, rcap);
+        // RCP: exact reciprocal-fma division with r = 1/c from the LDS table; wide stations
+        // (no table, see StepLds) divide directly -- both are the IEEE quotient
+        change = RCP ? div_by_cap((double)pdt, cap, rcap) : (double)pdt / cap;
     }
     const double calc = prev + change;
     double pw_dis = pc;                                          // inverted flag, charger.py:122-132
@@ -477,8 +479,11 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
 __host__ __device__ constexpr int step_block(int NC) { return (NC > 0 && NC <= 16) ? 256 : 64; }
 
 // LDS carve-up of the step kernel, one slice per wavefront (every region 16-byte aligned):
-//   act [WENVS][A] f32 | obs [WENVS][O] f32 | rcp [256] f64 | cst [16] f64
-//   | pos [WENVS][NC] f64 | neg [WENVS][NC] f64 | (L > 1) pw [WENVS][NC] f64 | q [WENVS][NC] f64
+//   act [WENVS][A] f32 | obs [WENVS][O] f32 | (kRows) rcp [256] f64 | (kRows) cst [16] f64
+//   | pos [WENVS][NC] f64 | neg [WENVS][NC] f64 | (L > 1) pw [WENVS][NC] f64
+// With L > 1 the penalty rows q [WENVS][NC] f64 share the first region with the actions tile:
+// a lane's chargers are one batch, whose action reads all precede the first q write in the
+// wavefront's program order (the BESS action is read before the loop).
 // Each wavefront stages, computes and writes back its own 64/L envs: no workgroup barrier, so
 // the waves of a CU drift apart and one wave's loads overlap another's arithmetic and stores.
 template <int NC, int L>
@@ -490,10 +495,17 @@ struct StepLds {
     static constexpr bool kRows = NC > 0 && NC <= 16;   // compacted power rows (else PairwiseSum)
     __host__ __device__ static int act_floats(int A) { return round4(WENVS * A); }
     __host__ __device__ static int obs_floats(int O) { return round4(WENVS * O); }
+    // wide stations (!kRows) keep no 1/c table and no step constants in LDS: at N = 50 the act
+    // and obs tiles alone are 40 KB per wavefront, and 40 KB is what lets 4 wavefronts (one per
+    // SIMD) share a CU's 160 KB
+    __host__ __device__ static size_t first_bytes(int A) {   // actions tile, or the q rows aliasing it
+        const size_t a = (size_t)act_floats(A) * 4, q = L > 1 ? (size_t)WENVS * NC * 8 : 0;
+        return a > q ? a : q;
+    }
     __host__ __device__ static size_t wave_bytes(int A, int O) {
-        size_t b = (size_t)(act_floats(A) + obs_floats(O)) * 4 + (256 + 16) * 8;
-        if (kRows) b += (size_t)2 * WENVS * NC * 8;
-        if (L > 1) b += (size_t)2 * WENVS * NC * 8;
+        size_t b = first_bytes(A) + (size_t)obs_floats(O) * 4;
+        if (kRows) b += (size_t)(256 + 16) * 8 + (size_t)2 * WENVS * NC * 8;
+        if (L > 1) b += (size_t)WENVS * NC * 8;
         return b;
     }
     __host__ __device__ static size_t bytes(int A, int O) { return WAVES * wave_bytes(A, O); }
@@ -540,13 +552,13 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     const bool live = le < nw;
     const bool leader = part == 0;
     float *s_act = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + wave * Lay::wave_bytes(A, O));
-    float *s_obs = s_act + Lay::act_floats(A);
-    double *s_rcp = reinterpret_cast<double *>(s_obs + Lay::obs_floats(O));
-    double *s_cst = s_rcp + 256;                                  // [16] per-step constants (CST_*)
-    double *s_pos = s_cst + 16;                                   // [WENVS][NC] compacted positive powers
+    float *s_obs = reinterpret_cast<float *>(reinterpret_cast<char *>(s_act) + Lay::first_bytes(A));
+    double *s_rcp = reinterpret_cast<double *>(s_obs + Lay::obs_floats(O));   // [256] 1/c (kRows)
+    double *s_cst = s_rcp + (kRows ? 256 : 0);                    // [16] per-step constants (kRows)
+    double *s_pos = s_cst + (kRows ? 16 : 0);                     // [WENVS][NC] compacted positive powers
     double *s_neg = s_pos + (kRows ? WENVS * NC : 0);             // [WENVS][NC] compacted negative powers
     double *s_pw = s_neg + (kRows ? WENVS * NC : 0);              // [WENVS][NC] per-charger powers (L > 1)
-    double *s_q = s_pw + (L > 1 ? WENVS * NC : 0);                // [WENVS][NC] per-charger penalty terms
+    double *s_q = reinterpret_cast<double *>(s_act);              // [WENVS][NC] penalty terms (L > 1)
     const uint32_t *__restrict__ word = s.word;
     const double *__restrict__ auxv = s.aux;
     const double *__restrict__ reqv = s.req;
@@ -617,11 +629,17 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         }
     }
     // 3. tables and the wave's actions tile
-    constexpr int RCP_PER_LANE = 256 / kWave;
-    double rcp_v[RCP_PER_LANE];
+    //    (wide stations: no 1/c table, the step constants in scalar registers -- see StepLds)
+    constexpr int RCP_PER_LANE = kRows ? 256 / kWave : 0;
+    double rcp_v[RCP_PER_LANE > 0 ? RCP_PER_LANE : 1];
 #pragma unroll
     for (int k = 0; k < RCP_PER_LANE; ++k) rcp_v[k] = s.tables->recip[k * kWave + lane];
-    const double cst_v = (lane < CST_COUNT) ? step_constant(s.tables, t, lane) : 0.0;
+    const double cst_v = (kRows && lane < CST_COUNT) ? step_constant(s.tables, t, lane) : 0.0;
+    double cst_r[CST_COUNT];
+    if (!kRows) {
+#pragma unroll
+        for (int i = 0; i < CST_COUNT; ++i) cst_r[i] = step_constant(s.tables, t, i);   // uniform: s_load
+    }
     TileStage<KT, kWave> act_tile;
     act_tile.issue(act + e0 * A, nw * A, vec_io != 0, lane);
     // 4. per-charger state of the first batch
@@ -631,13 +649,15 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
 #endif
 #pragma unroll
     for (int k = 0; k < RCP_PER_LANE; ++k) s_rcp[k * kWave + lane] = rcp_v[k];
-    if (lane < CST_COUNT) s_cst[lane] = cst_v;
+    if (kRows && lane < CST_COUNT) s_cst[lane] = cst_v;
+    const double *cst = kRows ? s_cst : cst_r;
     act_tile.commit(s_act, lane);
     wave_lds_fence();
     SNG_STAMP(1);
 
     const float *a_row = s_act + le * A;
     float *o_row = s_obs + le * O;
+    const float bess_action = p.bess ? a_row[n] : 0.0f;   // before the q rows reuse the tile
     const int k_soc = (p.pv ? 8 : 4);
     PairwiseSum pos, neg;
     double seq_pos = 0.0, seq_neg = 0.0;
@@ -681,13 +701,14 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
                 av[j] = (c < cend) ? a_row[c] : 0.0f;
-                rc[j] = s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu];
+                rc[j] = kRows ? s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu] : 0.0;
             }
+            if (L > 1) wave_lds_fence();   // the q rows below reuse the actions tile
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
                 if (c >= cend) break;
-                const ChargerResult r = charger_step<FAST>(p, w[j], aux[j], run[j], req[j], av[j], t, rc[j]);
+                const ChargerResult r = charger_step<FAST, kRows>(p, w[j], aux[j], run[j], req[j], av[j], t, rc[j]);
                 SNG_ST(socv[(size_t)c * E + e], r.soc);
                 if (DIAG) {   // 'Charger power values' and the SOC[c, t] the day record holds
                     if (info.charger_power) info.charger_power[(size_t)e * n + c] = r.pw;
@@ -756,9 +777,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             p_ch = pos.result();
             p_dis = neg.result();
         }
-        env_tail<DIAG>(p, s, info, e, t, ratio, bess, p.bess ? a_row[n] : 0.0f, p_ch, p_dis, pen_v,
+        env_tail<DIAG>(p, s, info, e, t, ratio, bess, bess_action, p_ch, p_dis, pen_v,
                        100.0 * (double)n_nonexist, fl,
-                       o_row, s_cst, fpv, fpr, ret_prev, bess0, reward, done);
+                       o_row, cst, fpv, fpr, ret_prev, bess0, reward, done);
     }
     wave_lds_fence();
     SNG_STAMP(2);
