@@ -955,6 +955,12 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     double req_cur = (nv > 0 && p.req_enabled) ? s_req[tid] : 1.0;
     bool prev_occ = false;
     int prev_rem = 0;
+    // penalty-check list built by observe(t-1) (charging_station.py:42-63) as one unsigned range
+    // test on the steps the vehicle at t-1 had left: on_departure {1}, sparse {1..3}, dense any;
+    // no_penalty never (lo = 256 > any remainder)
+    const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;
+    const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
+                              : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
     for (int t = 0; t < T; ++t) {
         if (t > (int)((cur >> 8) & 0xffu) && v < nv) {   // past the current departure: next vehicle
             ++v;
@@ -966,16 +972,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const uint32_t cap = (cur >> 16) & 0xffu;
         const bool occ = t >= ta && t < dep;
         const bool arrived = t == ta;
-        // penalty-check list built by observe(t-1) (charging_station.py:42-63)
-        bool pen = false;
-        if (t > 0 && prev_occ) {
-            switch (p.penalty_mode) {
-                case SNG_PENALTY_ON_DEPARTURE: pen = (prev_rem == 1); break;
-                case SNG_PENALTY_SPARSE: pen = (prev_rem >= 1 && prev_rem <= 3); break;
-                case SNG_PENALTY_DENSE: pen = true; break;
-                default: pen = false;
-            }
-        }
+        const bool pen = (uint32_t)prev_rem - pen_lo <= pen_span;   // prev_rem = 0: charger empty at t-1
         const int rem = occ ? dep - t : 0;
         // row base is wave-uniform (scalar), the lane adds a 32-bit offset
         const size_t row = ((size_t)t * n + c) * (size_t)E;
