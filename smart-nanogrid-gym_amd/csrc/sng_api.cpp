@@ -530,6 +530,11 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
     int rc = validate(cfg, &T, err);
     if (rc) return fail(nullptr, rc, err);
     if (num_envs < 1) return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "num_envs must be >= 1");
+    // the step kernel addresses a charger-major plane ([N][E] f64: the SoC state, one timestep of
+    // the timeline) as one raw buffer with 32-bit byte offsets
+    if ((uint64_t)num_envs * (uint64_t)cfg->number_of_chargers * sizeof(double) >= (1ull << 32))
+        return fail(nullptr, SNG_ERR_INVALID_ARGUMENT,
+                    "num_envs * number_of_chargers must be < 2^29 per handle (shard larger populations)");
 
     SngEnv *env = new SngEnv();
     env->cfg = *cfg;

@@ -30,23 +30,6 @@ constexpr int kWave = 64;
 // Streaming (nontemporal) stores for the step's bulk outputs (SoC, observations): they leave
 // less dirty L2 for the end-of-kernel release (measured 8.92 -> 8.17 us per step at 65,536 x 10).
 #define SNG_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
-// Streaming loads for the scenario timeline (read once per day): experiment switch.
-#ifdef SNG_NT_LOADS
-#define SNG_LD(src) __builtin_nontemporal_load(&(src))
-#else
-#define SNG_LD(src) (src)
-#endif
-#ifdef SNG_NT_GEN
-#define SNG_GST(dst, v) __builtin_nontemporal_store((v), &(dst))
-#else
-#define SNG_GST(dst, v) ((dst) = (v))
-#endif
-#ifdef SNG_NT_LOADS_SOC
-#define SNG_LDS(src) __builtin_nontemporal_load(&(src))
-#else
-#define SNG_LDS(src) (src)
-#endif
-
 #ifdef SNG_STAMPS
 // Diagnostic build only (make stamps): per-workgroup s_memrealtime stamps (100 MHz) at the
 // phase boundaries of the step kernel -> g_stamps[block*4 + k].  Never compiled into libsng.so.
@@ -119,6 +102,35 @@ __device__ __forceinline__ double pairwise_row(const double *row, int n, double 
 }
 
 __host__ __device__ constexpr int round4(int x) { return (x + 3) & ~3; }
+
+// Raw buffer access: V# = an array (or a per-step timeline plane) in SGPRs, a wave-uniform
+// byte offset (soffset, e.g. the charger row) and a per-lane 32-bit byte offset (the env).  The
+// adds happen in the buffer unit instead of as 64-bit VALU adds per access.  Every array or plane
+// addressed this way is < 4 GiB (checked at sng_create).  dword3 0x00020000: gfx9 raw buffer.
+using Rsrc = __amdgpu_buffer_rsrc_t;
+__device__ __forceinline__ Rsrc rsrc(const void *base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, -1, 0x00020000);
+}
+constexpr int kNT = 2;   // buffer cache-policy bit: nontemporal (streaming) access
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+template <class T, int POL = 0>
+__device__ __forceinline__ T bld(const T *base, uint32_t voff, uint32_t soff = 0) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4 or 8 byte elements");
+    if constexpr (sizeof(T) == 8)
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b64(rsrc(base), voff, soff, POL));
+    else
+        return __builtin_bit_cast(T, __builtin_amdgcn_raw_buffer_load_b32(rsrc(base), voff, soff, POL));
+}
+template <int POL = 0, class T>
+__device__ __forceinline__ void bst(T *base, uint32_t voff, T v, uint32_t soff = 0) {
+    static_assert(sizeof(T) == 1 || sizeof(T) == 4 || sizeof(T) == 8, "1, 4 or 8 byte elements");
+    if constexpr (sizeof(T) == 8)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, v), rsrc(base), voff, soff, POL);
+    else if constexpr (sizeof(T) == 4)
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rsrc(base), voff, soff, POL);
+    else
+        __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(unsigned char, v), rsrc(base), voff, soff, POL);
+}
 
 // Copy `count` floats global -> LDS with 16 B per lane when the run is aligned.  Each thread
 // issues up to K loads before the first LDS write (clamped, unconditional loads: no per-element
@@ -392,7 +404,7 @@ __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t 
 // accountant.py:213-227) and the observation header.  Leader lane only.
 // ---------------------------------------------------------------------------------
 template <bool DIAG>
-__device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, const InfoPtrs &info, int64_t e,
+__device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, const InfoPtrs &info, int64_t e0, uint32_t lo, uint32_t el1, uint32_t el8,
                                          int t, double ratio, double bess, float bess_action, double p_ch,
                                          double p_dis, double pen_v, double nonexist, uint32_t fl, float *o_row,
                                          const double *cst, const double *fpv, const double *fpr, double ret_prev,
@@ -406,7 +418,7 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     double pen_b = 0.0, bpow = 0.0, bcalc = 0.0;
     if (p.bess) {
         if (t == 0) {                                              // :93-94
-            s.bess0[e] = bess;
+            bst(s.bess0, el8, bess);
             bess0 = bess;
         }
         const double ba = (double)bess_action;
@@ -438,7 +450,7 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
         } else if (!(bess <= 1.0)) {
             fl |= SNG_FLAG_BESS_SOC_ABOVE_1;
         }
-        SNG_ST(s.bess[e], bess);
+        bst<kNT>(s.bess, el8, bess);
     }
 
     const double grid = rem;
@@ -447,29 +459,29 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     const double cost = (energy < 0.0) ? (energy * p.sell_coef) * price : energy * price;
     const double tot_pen = p.bat_pen_w * pen_b + pen_v;
     const double total = p.grid_w * fabs(cost) + tot_pen;
-    SNG_ST(reward[e], -total);
-    SNG_ST(done[e], (uint8_t)((t + 1 == p.T) ? 1 : 0));
+    bst<kNT>(reward, el8, -total);
+    bst<kNT>(done, el1, (uint8_t)((t + 1 == p.T) ? 1 : 0));
 
     write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio, fpv, fpr);
     if (p.bess) o_row[p.obs_dim - 1] = (float)bess;
 
-    if (fl) atomicOr(&s.flags[e], fl);   // rare (sticky error bits); no-return atomic, nothing waits
-    if (info.flags) info.flags[e] = fl;
-    if (info.episode_return) SNG_ST(info.episode_return[e], ret_prev + -total);
+    if (fl) atomicOr(s.flags + e0 + lo, fl);   // rare (sticky error bits); no-return atomic, nothing waits
+    if (info.flags) bst(info.flags, el1 * 4u, fl);
+    if (info.episode_return) bst<kNT>(info.episode_return, el8, ret_prev + -total);
     if (DIAG) {
-        if (info.grid_power) info.grid_power[e] = grid;
-        if (info.p_charge) info.p_charge[e] = p_ch;
-        if (info.p_discharge) info.p_discharge[e] = p_dis;
-        if (info.bess_soc) info.bess_soc[e] = p.bess ? bess : 0.0;
-        if (info.pen_vehicle) info.pen_vehicle[e] = pen_v;
-        if (info.pen_battery) info.pen_battery[e] = pen_b;
-        if (info.grid_cost) info.grid_cost[e] = cost;
-        if (info.total_cost) info.total_cost[e] = total;
-        if (info.solar) info.solar[e] = solar;
-        if (info.bess_power) info.bess_power[e] = bpow;
-        if (info.bess_calc_power) info.bess_calc_power[e] = bcalc;
-        if (info.nonexistent) info.nonexistent[e] = nonexist;
-        if (info.bess_initial) info.bess_initial[e] = p.bess ? bess0 : 0.0;
+        if (info.grid_power) bst(info.grid_power, el8, (double)(grid));
+        if (info.p_charge) bst(info.p_charge, el8, (double)(p_ch));
+        if (info.p_discharge) bst(info.p_discharge, el8, (double)(p_dis));
+        if (info.bess_soc) bst(info.bess_soc, el8, (double)(p.bess ? bess : 0.0));
+        if (info.pen_vehicle) bst(info.pen_vehicle, el8, (double)(pen_v));
+        if (info.pen_battery) bst(info.pen_battery, el8, (double)(pen_b));
+        if (info.grid_cost) bst(info.grid_cost, el8, (double)(cost));
+        if (info.total_cost) bst(info.total_cost, el8, (double)(total));
+        if (info.solar) bst(info.solar, el8, (double)(solar));
+        if (info.bess_power) bst(info.bess_power, el8, (double)(bpow));
+        if (info.bess_calc_power) bst(info.bess_calc_power, el8, (double)(bcalc));
+        if (info.nonexistent) bst(info.nonexistent, el8, (double)(nonexist));
+        if (info.bess_initial) bst(info.bess_initial, el8, (double)(p.bess ? bess0 : 0.0));
     }
 }
 
@@ -543,7 +555,8 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int n = NC ? NC : p.n;
     const int A = p.act_dim, O = p.obs_dim;
-    const int wave = threadIdx.x / kWave, lane = threadIdx.x % kWave;
+    // the wavefront index is wave-uniform: readfirstlane keeps e0 and the row offsets scalar
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const int le = lane / L, part = lane % L;
     const int64_t e0 = (int64_t)blockIdx.x * Lay::ENVS + (int64_t)wave * WENVS;   // this wave's first env
     if (e0 >= E) return;                                                           // wave-uniform
@@ -573,6 +586,11 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     // vmcnt(#per-charger loads) and charger c's update starts as soon as its own loads land.
     // Non-live lanes load a valid env (E - 1) and discard it.
     const int64_t el = live ? e : E - 1;
+    const uint32_t lo = (uint32_t)(el - e0);   // lane offset from the wave's first env
+    const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;   // byte offsets of the env
+    const uint32_t *__restrict__ word_t = word + tbase * (size_t)E;   // this step's timeline planes
+    const double *__restrict__ aux_t = auxv + tbase * (size_t)E;
+    const double *__restrict__ req_t = reqv + tbase * (size_t)E;
     uint32_t w[CH];
     double aux[CH], run[CH], req[CH];
     auto load_state = [&](int c0) {
@@ -580,10 +598,10 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         for (int j = 0; j < CH; ++j) {
             const int c = c0 + j;
             if (c < cend) {
-                const size_t idx = (tbase + c) * (size_t)E + el;
-                w[j] = SNG_LD(word[idx]);
-                aux[j] = SNG_LD(auxv[idx]);
-                run[j] = SNG_LDS(socv[(size_t)c * E + el]);
+                const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
+                w[j] = bld(word_t, el4, r4);
+                aux[j] = bld(aux_t, el8, r8);
+                run[j] = bld(socv, el8, r8);
             } else {
                 w[j] = 0u;
                 aux[j] = run[j] = 0.0;
@@ -595,7 +613,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
-                req[j] = (c < cend) ? reqv[(tbase + c) * (size_t)E + el] : 1.0;
+                req[j] = (c < cend) ? bld(req_t, el8, (uint32_t)c * (uint32_t)E * 8u) : 1.0;
             }
         } else {
 #pragma unroll
@@ -608,11 +626,11 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     };
 
     // 1. per-env values: pointer selects rather than branches (a disabled stream re-reads ratio)
-    const double ratio = s.ratio[el];
-    const double bess_l = (p.bess ? s.bess : s.ratio)[el];
-    const double pen0_l = (t == 0 ? s.pen0 : s.ratio)[el];
-    const double ret_l = (info.episode_return ? info.episode_return : s.ratio)[el];
-    const double bess0 = DIAG ? ((p.bess && t > 0 && info.bess_initial) ? s.bess0 : s.ratio)[el] : 0.0;
+    const double ratio = bld(s.ratio, el8);
+    const double bess_l = bld(p.bess ? s.bess : s.ratio, el8);
+    const double pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
+    const double ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
+    const double bess0 = DIAG ? bld((p.bess && t > 0 && info.bess_initial) ? s.bess0 : s.ratio, el8) : 0.0;
     const double bess = p.bess ? bess_l : 0.0;
     const double pen0 = (t == 0) ? pen0_l : 0.0;
     const double ret_prev = info.episode_return ? ret_l : 0.0;
@@ -624,8 +642,8 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         const size_t plane = (size_t)(p.T + 3) * E;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            fpv[j] = s.prof[(size_t)(t + j) * E + el];
-            fpr[j] = s.prof[plane + (size_t)(t + j) * E + el];
+            fpv[j] = bld(s.prof + (size_t)(t + j) * E, el8);
+            fpr[j] = bld(s.prof + plane + (size_t)(t + j) * E, el8);
         }
     }
     // 3. tables and the wave's actions tile
@@ -709,7 +727,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                 const int c = c0 + j;
                 if (c >= cend) break;
                 const ChargerResult r = charger_step<FAST, kRows>(p, w[j], aux[j], run[j], req[j], av[j], t, rc[j]);
-                SNG_ST(socv[(size_t)c * E + e], r.soc);
+                bst<kNT>(socv, el8, r.soc, (uint32_t)c * (uint32_t)E * 8u);
                 if (DIAG) {   // 'Charger power values' and the SOC[c, t] the day record holds
                     if (info.charger_power) info.charger_power[(size_t)e * n + c] = r.pw;
                     if (info.vehicle_soc) info.vehicle_soc[(size_t)e * n + c] = r.soc;
@@ -777,7 +795,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             p_ch = pos.result();
             p_dis = neg.result();
         }
-        env_tail<DIAG>(p, s, info, e, t, ratio, bess, bess_action, p_ch, p_dis, pen_v,
+        env_tail<DIAG>(p, s, info, e0, lo, el1, el8, t, ratio, bess, bess_action, p_ch, p_dis, pen_v,
                        100.0 * (double)n_nonexist, fl,
                        o_row, cst, fpv, fpr, ret_prev, bess0, reward, done);
     }
@@ -961,6 +979,8 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
+    const uint32_t el4 = (uint32_t)e * 4u, el8 = (uint32_t)e * 8u;
+    const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
     for (int t = 0; t < T; ++t) {
         if (t > (int)((cur >> 8) & 0xffu) && v < nv) {   // past the current departure: next vehicle
             ++v;
@@ -974,18 +994,18 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const bool arrived = t == ta;
         const bool pen = (uint32_t)prev_rem - pen_lo <= pen_span;   // prev_rem = 0: charger empty at t-1
         const int rem = occ ? dep - t : 0;
-        // row base is wave-uniform (scalar), the lane adds a 32-bit offset
-        const size_t row = ((size_t)t * n + c) * (size_t)E;
-        const uint32_t el = (uint32_t)e;
-        SNG_GST(s.word[row + el], pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem));
-        SNG_GST(s.aux[row + el], arrived ? soc_cur : 0.0);   // dense: full-line stores
+        // raw buffer stores: the step's plane in the V#, the charger row in soffset, the env in
+        // the 32-bit lane offset
+        const size_t plane = (size_t)t * n * (size_t)E;
+        bst(s.word + plane, el4, pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem), r4);
+        bst(s.aux + plane, el8, arrived ? soc_cur : 0.0, r8);   // dense: full-line stores
         // requested SoC timeline (sng_layout.h): Requested_SOC[c, t-1] at t >= 1 -- the step reads
         // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
-        if (p.req_stream && t > 0) SNG_GST(s.req[row + el], prev_occ ? req_cur : 0.0);
+        if (p.req_stream && t > 0) bst(s.req + plane, el8, prev_occ ? req_cur : 0.0, r8);
         prev_occ = occ;
         prev_rem = rem;
     }
-    if (p.req_stream) SNG_GST(s.req[(size_t)c * E + (uint32_t)e], prev_occ ? req_cur : 0.0);
+    if (p.req_stream) bst(s.req, el8, prev_occ ? req_cur : 0.0, r8);
     if (c == 0) {
         HashStream r2{stream_key(seed, ge, 0x7a710000u, day), 0u};            // the PV-ratio domain
         s.ratio[e] = (double)below(r2.next(), 181) / 100;   // random.randint(0, 180) / 100
