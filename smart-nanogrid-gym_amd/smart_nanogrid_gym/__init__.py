@@ -6,12 +6,15 @@
 with the reference's id and max_episode_steps (smart_nanogrid_gym/__init__.py:4-8).
 """
 from .envs import SmartNanogridEnv
+from .evaluation import (RuleBasedController, evaluate_model_for_single_episode, evaluate_models, generate_days,
+                         predict_single_day)
 from .recorder import DayRecorder
 from .settings import EnvSettings, parse_time_interval
 from .vec_env import EpisodeGraph, SmartNanogridVecEnv
 
 __all__ = ["SmartNanogridEnv", "SmartNanogridVecEnv", "EpisodeGraph", "EnvSettings", "DayRecorder",
-           "parse_time_interval"]
+           "parse_time_interval", "RuleBasedController", "evaluate_model_for_single_episode", "predict_single_day",
+           "evaluate_models", "generate_days"]
 
 
 def _register():
