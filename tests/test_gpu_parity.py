@@ -316,6 +316,38 @@ def test_sharded_population_reproduces_single_gpu(rng):
         v.close()
 
 
+def test_config4_full_size_eight_shards_reproduce_one_population():
+    """BASELINE config 4 (262,144 envs x 10 chargers over 8 GPUs, 32,768 per GPU) at full size on
+    one GPU: the 8 shard handles a world-8 run holds (env_offset r * 32,768) step bit for bit like
+    one 262,144-env handle, so the RCCL all-gather of their day returns is the single population's
+    returns.  Device RNG (the bench's resets), two days."""
+    W, E, N = 8, 32768, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    full = SmartNanogridVecEnv(W * E, seed=2024, rng="device", **kw)
+    shards = [SmartNanogridVecEnv(E, seed=2024, rng="device", env_offset=r * E, **kw) for r in range(W)]
+    g = torch.Generator(device="cuda:0").manual_seed(11)
+    for day in range(2):
+        of = full.reset_tensors().clone()
+        os_ = torch.cat([sh.reset_tensors().clone() for sh in shards])
+        assert torch.equal(of, os_)
+        for t in range(24):
+            a = torch.rand((W * E, N + 1), generator=g, device="cuda:0")
+            a[:, -1] = a[:, -1] * 2 - 1
+            a = torch.where(torch.rand(a.shape, generator=g, device="cuda:0") < 0.2, torch.zeros_like(a), a)
+            o, r, d = full.step_tensors(a)
+            parts = [sh.step_tensors(a[k * E:(k + 1) * E].contiguous()) for k, sh in enumerate(shards)]
+            assert torch.equal(o, torch.cat([p[0] for p in parts]))
+            assert torch.equal(r, torch.cat([p[1] for p in parts]))
+            assert torch.equal(d, torch.cat([p[2] for p in parts]))
+        gathered = torch.cat([sh.return_d for sh in shards])
+        assert torch.equal(full.return_d, gathered)
+        ret = gathered.cpu().numpy()
+        assert np.isfinite(ret).all() and (ret <= 0).all() and (ret < 0).mean() > 0.99
+    for v in [full] + shards:
+        v.close()
+
+
 CONFIG5 = dict(number_of_chargers=50, time_interval="15min", charging_mode="bounded",
                vehicle_uncharged_penalty_mode="sparse", extended_day=True, pv_noise=0.2, price_noise=0.1)
 
