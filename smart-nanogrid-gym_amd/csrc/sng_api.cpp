@@ -589,9 +589,9 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
         }
         p.lanes = c.step_lanes_per_env;
     } else {
-        // tuned on MI355X at E=65,536: 1 lane at N=10 (tools/gpu_session.sh sweep), 2 at N=50
-        // (74 vs 96 us per step, profiles/r01_bench_config5*.log)
-        p.lanes = (p.n > 16 && step_lanes_supported(p.n, 2)) ? 2 : 1;
+        // tuned on MI355X at E=65,536 (bench.py --lanes): 1 lane per env at N=10 (7.6 / 8.9 / 11.4 us
+        // for 1 / 2 / 4 lanes) and at N=50, config 5 (38.9 / 42.1 / 51.9 us)
+        p.lanes = 1;
     }
     env->i4 = (int)(4 / p.dt);
     env->i10 = (int)(10 / p.dt);

@@ -523,6 +523,17 @@ struct StepLds {
     __host__ __device__ static size_t bytes(int A, int O) { return WAVES * wave_bytes(A, O); }
 };
 
+// Chargers per batch of the one-lane step kernel: all of them up to 16; for wider stations the
+// largest divisor of N in [10, 16] (no ragged last batch), else 8 -- each batch's loads are issued
+// together and then consumed.  Measured at N = 50 (config 5): batches of 10 33.1 us per step, 17
+// 33.5, 25 34.5, 13 36.8, 8 39.1.
+__host__ __device__ constexpr int wide_batch(int NC) {
+    if (NC > 0 && NC <= 16) return NC;
+    for (int d = 16; d >= 10; --d)
+        if (NC > 0 && NC % d == 0) return d;
+    return 8;
+}
+
 // LDS ordering inside one wavefront: a wave's LDS operations complete in issue order, so a
 // compiler-level fence is all that is needed between the writes of some lanes and the reads of
 // others (no s_barrier).
@@ -549,7 +560,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     using Lay = StepLds<NC, L>;
     constexpr int WENVS = Lay::WENVS;
     constexpr bool kRows = Lay::kRows;
-    constexpr int CH = (L > 1) ? (NC + L - 1) / L : ((NC > 0 && NC <= 16) ? NC : 8);
+    constexpr int CH = (L > 1) ? (NC + L - 1) / L : wide_batch(NC);
     // actions tile in one round: K float4 per lane covers WENVS * A floats for A <= NC + 1
     constexpr int KT = NC > 0 ? ((NC + 1) * WENVS + 4 * kWave - 1) / (4 * kWave) : 8;
     extern __shared__ __attribute__((aligned(16))) float lds[];
