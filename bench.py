@@ -34,11 +34,12 @@ METRIC = "env-steps/sec (whole node) at N=65,536 envs × 10 chargers, 24-step da
 
 
 def step_kernel_bytes(n, noise=False):
-    """Algorithmic bytes one env moves in one fused step (b-pv, no requested-SoC stream):
-    actions 4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N + scenario word 4N
-    + static SoC 8N + BESS r/w 16 + PV ratio 8 + day-return r/w 16 = 40N + 89
-    (+ 64 for the PV / price profile factors of t..t+3 with stochastic profiles)."""
-    return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 4 * n + 8 * n + 16 + 8 + 16 + (64 if noise else 0)
+    """Algorithmic bytes one env moves in one fused step of a device-RNG day (b-pv, no
+    requested-SoC stream): actions 4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N
+    + packed charger-step record 8N (scenario word + float32 static SoC) + BESS r/w 16 + PV ratio 8
+    + day-return r/w 16 = 36N + 89 (+ 64 for the PV / price profile factors of t..t+3 with
+    stochastic profiles).  Host-RNG days read the word and a float64 static SoC instead: 40N + 89."""
+    return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 8 * n + 16 + 8 + 16 + (64 if noise else 0)
 
 
 def cpu_baseline(kw, budget_s):
@@ -192,7 +193,7 @@ def main():
         launch_s = float(np.mean(kernel_ms)) / 1e3
         bpl = step_kernel_bytes(N, noise) * E
         achieved = bpl / launch_s / 1e9
-        kernel = f"void sng::step_kernel<{N}, {venv.step_lanes}, false, true>"
+        kernel = f"void sng::step_kernel<{N}, {venv.step_lanes}, false, true, true>"
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N, kernel),
                 "kernel": kernel, "bytes_per_launch": bpl,

@@ -356,6 +356,8 @@ struct SngEnv {
 
 struct SngGraph {
     SngEnv *env = nullptr;
+    bool with_reset = false;
+    int packed = 0;   // the timeline encoding the graph's steps read
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
 };
@@ -440,6 +442,7 @@ int upload_and_observe(SngEnv *env, bool need_req, float *obs, hipStream_t st) {
     HIP_TRY(env, hipMemcpyAsync(env->ds.pen0, env->h_pen0, env->E * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipEventRecord(env->staging_done, st));
     env->p.req_stream = need_req ? 1 : 0;
+    env->p.packed = 0;   // word + f64 aux planes
     HIP_TRY(env, sng::launch_profiles(env->p, env->ds, env->E, st));
     HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st));
     env->t = 0;
@@ -711,6 +714,7 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     if (rng_mode == SNG_RNG_DEVICE) {
         if (!device_rng_ok(env)) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
         env->p.req_stream = env->p.req_enabled;
+        env->p.packed = 1;   // the generator writes packed records (sng_layout.h)
         if (env->p.req_stream) {
             int rc = ensure_req(env);
             if (rc) return rc;
@@ -887,10 +891,23 @@ int sng_get_scenario(SngEnv *env, int64_t e, int32_t V, double *soc, double *occ
     const size_t rows = (size_t)T * N, pitch = (size_t)env->E;
     std::vector<uint32_t> w(rows);
     std::vector<double> aux(rows), rq;
-    HIP_TRY(env, hipMemcpy2D(w.data(), sizeof(uint32_t), env->ds.word + e, pitch * sizeof(uint32_t), sizeof(uint32_t),
-                             rows, hipMemcpyDeviceToHost));
-    HIP_TRY(env, hipMemcpy2D(aux.data(), sizeof(double), env->ds.aux + e, pitch * sizeof(double), sizeof(double), rows,
-                             hipMemcpyDeviceToHost));
+    if (env->p.packed) {   // device-RNG day: packed records in the aux buffer (sng_layout.h)
+        std::vector<uint64_t> rec(rows);
+        HIP_TRY(env, hipMemcpy2D(rec.data(), sizeof(uint64_t), reinterpret_cast<const uint64_t *>(env->ds.aux) + e,
+                                 pitch * sizeof(uint64_t), sizeof(uint64_t), rows, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < rows; ++i) {
+            w[i] = (uint32_t)rec[i];
+            const uint32_t hi = (uint32_t)(rec[i] >> 32);
+            float f;
+            std::memcpy(&f, &hi, sizeof f);
+            aux[i] = (double)f;
+        }
+    } else {
+        HIP_TRY(env, hipMemcpy2D(w.data(), sizeof(uint32_t), env->ds.word + e, pitch * sizeof(uint32_t),
+                                 sizeof(uint32_t), rows, hipMemcpyDeviceToHost));
+        HIP_TRY(env, hipMemcpy2D(aux.data(), sizeof(double), env->ds.aux + e, pitch * sizeof(double), sizeof(double),
+                                 rows, hipMemcpyDeviceToHost));
+    }
     const bool have_req = env->p.req_stream && env->ds.req;
     if (have_req) {
         rq.resize(rows);
@@ -966,7 +983,12 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
     SngGraph *g = new SngGraph();
     g->env = env;
     Params p = env->p;
-    if (with_reset) p.req_stream = p.req_enabled;
+    if (with_reset) {
+        p.req_stream = p.req_enabled;
+        p.packed = 1;
+    }
+    g->with_reset = with_reset;
+    g->packed = p.packed;
     const InfoPtrs ip = info_ptrs(info);
     const int64_t E = env->E;
     const int A = p.act_dim;
@@ -1001,8 +1023,14 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
 int sng_graph_launch(SngGraph *g, void *stream) {
     if (!g) return SNG_ERR_INVALID_ARGUMENT;
     SngEnv *env = g->env;
+    if (!g->with_reset && g->packed != env->p.packed)
+        return fail(env, SNG_ERR_STATE, "graph captured for days of the other RNG mode: recapture it after this reset");
     HIP_TRY(env, hipSetDevice(env->device));
     HIP_TRY(env, hipGraphLaunch(g->exec, (hipStream_t)stream));
+    if (g->with_reset) {
+        env->p.req_stream = env->p.req_enabled;
+        env->p.packed = 1;
+    }
     env->t = env->p.T;
     env->day_finished = true;
     return SNG_OK;
@@ -1025,6 +1053,7 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     hipStream_t st = (hipStream_t)stream;
     Params p = env->p;
     p.req_stream = p.req_enabled;
+    p.packed = 1;
     if (p.req_stream) {
         int rc = ensure_req(env);
         if (rc) return rc;
@@ -1051,6 +1080,8 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     for (auto x : ev)
         if (x) (void)hipEventDestroy(x);
     if (e != hipSuccess) return hip_fail(env, e, "timed day");
+    env->p.req_stream = p.req_stream;
+    env->p.packed = 1;
     env->t = T;
     env->day_finished = true;
     return SNG_OK;

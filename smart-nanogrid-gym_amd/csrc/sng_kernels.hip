@@ -551,7 +551,7 @@ __device__ __forceinline__ void wave_lds_fence() {
 // Every per-charger load of a lane's batch is issued before any of it is used, and the first
 // batch before the action staging wait, so one lane keeps 3*CH + 2 requests in flight.
 // ---------------------------------------------------------------------------------
-template <int NC, int L, bool DIAG, bool FAST>
+template <int NC, int L, bool DIAG, bool FAST, bool PK>
 __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceState s, InfoPtrs info,
                                                               const float *__restrict__ act, float *__restrict__ obs,
                                                               double *__restrict__ reward, uint8_t *__restrict__ done,
@@ -610,8 +610,14 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             const int c = c0 + j;
             if (c < cend) {
                 const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
-                w[j] = bld(word_t, el4, r4);
-                aux[j] = bld(aux_t, el8, r8);
+                if (PK) {   // packed device-day record: word | float32 aux << 32 (sng_layout.h)
+                    const uint64_t rec = bld(reinterpret_cast<const uint64_t *>(aux_t), el8, r8);
+                    w[j] = (uint32_t)rec;
+                    aux[j] = (double)__uint_as_float((uint32_t)(rec >> 32));
+                } else {
+                    w[j] = bld(word_t, el4, r4);
+                    aux[j] = bld(aux_t, el8, r8);
+                }
                 run[j] = bld(socv, el8, r8);
             } else {
                 w[j] = 0u;
@@ -820,7 +826,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
 // Observation at t = 0 after a reset (SmartNanogridEnv.reset -> __get_observations,
 // smart_nanogrid_environment.py:358-360): SOC[c, 0] as generated, departure times at 0.
 // ---------------------------------------------------------------------------------
-template <int BLOCK>
+template <int BLOCK, bool PK>
 __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s, float *__restrict__ obs,
                                                          double *__restrict__ ep_return, int64_t E, int vec_io) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -853,8 +859,14 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int c = c0 + j < n ? c0 + j : n - 1;
-                w[j] = word[(size_t)c * E + e];
-                aux[j] = auxv[(size_t)c * E + e];
+                if (PK) {   // packed device-day record (sng_layout.h)
+                    const uint64_t rec = reinterpret_cast<const uint64_t *>(auxv)[(size_t)c * E + e];
+                    w[j] = (uint32_t)rec;
+                    aux[j] = (double)__uint_as_float((uint32_t)(rec >> 32));
+                } else {
+                    w[j] = word[(size_t)c * E + e];
+                    aux[j] = auxv[(size_t)c * E + e];
+                }
             }
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -900,7 +912,7 @@ __global__ __launch_bounds__(256) void profile_kernel(Params p, DeviceState s, i
 // with counter-based 32-bit hash streams, one per (global env, charger, day): draw i of a
 // stream is mix32(key + i * golden), three 32-bit multiplies (the earlier 64-bit SplitMix
 // streams cost ~4x the VALU; the kernel is bound by its dense timeline stores otherwise).
-// Thread = (env, charger); writes the dense word / aux (/ req) timeline.
+// Thread = (env, charger); writes the dense packed-record (/ req) timeline.
 // ---------------------------------------------------------------------------------
 struct HashStream {
     uint32_t key, ctr;
@@ -957,7 +969,8 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const float u = ((float)(rng.next() >> 8) + 1.0f) * 0x1.0p-24f;   // (0, 1]
         const int ta = tfree + (int)(__log2f(u) * kInvLog2Q);             // floor: the product is >= 0
         if (ta >= T) break;
-        const double soc_arr = 0.1 + (0.9 - 0.1) * u32_unit(rng.next());   // uniform(0.1, 0.9)
+        // uniform(0.1, 0.9), drawn as a float32 value (the packed record holds it exactly)
+        const double soc_arr = (double)(float)(0.1 + (0.9 - 0.1) * u32_unit(rng.next()));
         // capacity and departure from one draw: cap = floor(y * 105 / 2^32); the low word of
         // y * 105 (a bijection of y, uniform given cap) drives the departure
         const uint32_t y = rng.next();
@@ -1008,8 +1021,10 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         // raw buffer stores: the step's plane in the V#, the charger row in soffset, the env in
         // the 32-bit lane offset
         const size_t plane = (size_t)t * n * (size_t)E;
-        bst(s.word + plane, el4, pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem), r4);
-        bst(s.aux + plane, el8, arrived ? soc_cur : 0.0, r8);   // dense: full-line stores
+        // packed record (sng_layout.h): word | float32 bits of the aux value << 32, dense
+        const uint32_t word = pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem);
+        const uint64_t rec = (uint64_t)word | ((uint64_t)__float_as_uint(arrived ? (float)soc_cur : 0.0f) << 32);
+        bst(reinterpret_cast<uint64_t *>(s.aux) + plane, el8, rec, r8);
         // requested SoC timeline (sng_layout.h): Requested_SOC[c, t-1] at t >= 1 -- the step reads
         // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
         if (p.req_stream && t > 0) bst(s.req + plane, el8, prev_occ ? req_cur : 0.0, r8);
@@ -1040,7 +1055,9 @@ static void launch_step_t(const Params &p, const DeviceState &s, const InfoPtrs 
     using Lay = StepLds<NC, L>;
     const dim3 grid((unsigned)((E + Lay::ENVS - 1) / Lay::ENVS)), block(Lay::BLOCK);
     const uint32_t lds = (uint32_t)Lay::bytes(p.act_dim, p.obs_dim);
-    auto kern = (!p.legacy && p.dt_pow2) ? step_kernel<NC, L, DIAG, true> : step_kernel<NC, L, DIAG, false>;
+    const bool fast = !p.legacy && p.dt_pow2;
+    auto kern = p.packed ? (fast ? step_kernel<NC, L, DIAG, true, true> : step_kernel<NC, L, DIAG, false, true>)
+                         : (fast ? step_kernel<NC, L, DIAG, true, false> : step_kernel<NC, L, DIAG, false, false>);
     if (ev)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, p, s, info, act, obs, reward,
                               done, E, t, vec_io);
@@ -1106,12 +1123,14 @@ hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, do
                            int vec_io, hipStream_t stream) {
     if ((size_t)round4(256 * p.obs_dim) * 4 <= 64 * 1024) {
         const dim3 grid((unsigned)((E + 255) / 256)), block(256);
-        hipLaunchKernelGGL(observe0_kernel<256>, grid, block, (size_t)round4(256 * p.obs_dim) * 4, stream, p, s, obs,
-                           ep_return, E, vec_io);
+        auto kern = p.packed ? observe0_kernel<256, true> : observe0_kernel<256, false>;
+        hipLaunchKernelGGL(kern, grid, block, (size_t)round4(256 * p.obs_dim) * 4, stream, p, s, obs, ep_return, E,
+                           vec_io);
     } else {
         const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
-        hipLaunchKernelGGL(observe0_kernel<kWave>, grid, block, (size_t)round4(kWave * p.obs_dim) * 4, stream, p, s,
-                           obs, ep_return, E, vec_io);
+        auto kern = p.packed ? observe0_kernel<kWave, true> : observe0_kernel<kWave, false>;
+        hipLaunchKernelGGL(kern, grid, block, (size_t)round4(kWave * p.obs_dim) * 4, stream, p, s, obs, ep_return, E,
+                           vec_io);
     }
     return hipGetLastError();
 }

@@ -12,6 +12,10 @@
 //   aux    f64 [T][N][E]    per charger-step static SoC: the "previous" SoC when the word's
 //                           STATIC bit is set (arrival: SOC[c, t] as generated), else the
 //                           SOC[c, t] an unoccupied charger shows
+//   rec    u64 [T][N][E]    device-RNG days only, in the aux buffer (`word` unused): the packed
+//                           record word | float32 bits of the aux value << 32 -- one 8 B load or
+//                           store per charger-step instead of 12 B in two; the device generator
+//                           draws its arrival SoC as a float32 value, so the record is exact
 //   req    f64 [T][N][E]    Requested_SOC[c, t-1] (read by the penalty check where W_PEN is set);
 //                           the t = 0 slot, never read by a step, holds Requested_SOC[c, T-1] so the
 //                           day can be exported (sng_get_scenario); only when enabled
@@ -80,6 +84,7 @@ struct Params {
     int64_t env_offset;       // global index of env 0 of this handle (sharded runs)
     int32_t lanes;            // step kernel: lanes per environment (1, 2 or 4)
     int32_t noise;            // 1: stochastic PV / price profiles (DeviceState::prof is live)
+    int32_t packed;           // 1: the day's timeline is packed records in `aux` (device-RNG days)
     double pv_noise, price_noise;
     uint64_t seed;            // handle seed: env e's seed is seed + env_offset + e
 };
