@@ -260,6 +260,34 @@ def test_episode_graph_matches_eager_device_rng():
     b.close()
 
 
+def test_step_graph_follows_the_day_encoding():
+    """A steps-only graph (the T steps of a day, no reset) replays the day that is loaded:
+    device-RNG days are packed 8 B records, host-RNG days word + float64 planes (sng_layout.h).
+    Captured after a host-RNG reset it steps that day like eager steps; after a device-RNG reset
+    its replay is refused."""
+    from smart_nanogrid_gym._native import NativeError
+    E, N = 1024, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    a = SmartNanogridVecEnv(E, seed=3, rng="reference", **kw)
+    b = SmartNanogridVecEnv(E, seed=3, rng="reference", **kw)
+    a.reset_tensors()
+    b.reset_tensors()
+    day = EpisodeGraph(b, acts, with_reset=False)
+    for t in range(24):
+        oa, ra, _ = a.step_tensors(acts[t])
+    day.launch()
+    torch.cuda.synchronize()
+    assert torch.equal(oa, b.obs_d) and torch.equal(ra, b.reward_d)
+    b.reset_tensors(rng="device")
+    with pytest.raises(NativeError):
+        day.launch()
+    day.close()
+    a.close()
+    b.close()
+
+
 def test_single_env_gym_surface():
     env = SmartNanogridEnv(number_of_chargers=4, time_interval="1h", charging_mode="bounded",
                            vehicle_uncharged_penalty_mode="sparse", seed=12)
