@@ -369,9 +369,10 @@ int fail(SngEnv *env, int code, const std::string &msg) {
     return code;
 }
 
-// The device generator keeps up to 8 vehicles per charger and day in LDS (sng_kernels.hip,
-// kDayVehicles): a vehicle stays >= 4/dt steps and leaves one step empty.
-bool device_rng_ok(const SngEnv *env) { return env->i4 >= 2 && env->p.T / (env->i4 + 1) + 1 <= 8; }
+// The device generator keeps the day's vehicles of a charger plus an end sentinel in 8 LDS slots
+// (sng_kernels.hip, kDayVehicles): a vehicle stays >= 4/dt steps and leaves one step empty, so a
+// day has at most T / (4/dt + 1) + 1 vehicles, which must leave the sentinel's slot free.
+bool device_rng_ok(const SngEnv *env) { return env->i4 >= 2 && env->p.T / (env->i4 + 1) + 1 <= 7; }
 
 int hip_fail(SngEnv *env, hipError_t e, const char *what) {
     return fail(env, SNG_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));

@@ -964,7 +964,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
 
     // phase 1 (charging_station.py:200-279)
     int tfree = 0, nv = 0;
-    for (int v = 0; v < kDayVehicles; ++v) {
+    for (int v = 0; v < kDayVehicles - 1; ++v) {   // the last slot holds the sentinel
         if (tfree >= T) break;
         const float u = ((float)(rng.next() >> 8) + 1.0f) * 0x1.0p-24f;   // (0, 1]
         const int ta = tfree + (int)(__log2f(u) * kInvLog2Q);             // floor: the product is >= 0
@@ -990,11 +990,17 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         tfree = dep + 1;   // the departure step stays empty (charging_station.py:247-255)
     }
 
+    // slot nv: a sentinel that never arrives (arrival = departure = 255), so phase 2 walks the
+    // list without a per-step bound check or branch (nv <= 7 < kDayVehicles, checked on the host)
+    s_veh[nv * kGenBlock + tid] = 0xffffu;
+    s_soc[nv * kGenBlock + tid] = 0.0;
+    if (p.req_enabled) s_req[nv * kGenBlock + tid] = 1.0;
+
     // phase 2: the timeline
     int v = 0;
-    uint32_t cur = nv > 0 ? s_veh[tid] : 0xffu;   // arrival 255: no vehicle
-    double soc_cur = nv > 0 ? s_soc[tid] : 0.0;
-    double req_cur = (nv > 0 && p.req_enabled) ? s_req[tid] : 1.0;
+    uint32_t cur = s_veh[tid];
+    double soc_cur = s_soc[tid];
+    double req_cur = p.req_enabled ? s_req[tid] : 1.0;
     bool prev_occ = false;
     int prev_rem = 0;
     // penalty-check list built by observe(t-1) (charging_station.py:42-63) as one unsigned range
@@ -1006,12 +1012,10 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     const uint32_t el4 = (uint32_t)e * 4u, el8 = (uint32_t)e * 8u;
     const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
     for (int t = 0; t < T; ++t) {
-        if (t > (int)((cur >> 8) & 0xffu) && v < nv) {   // past the current departure: next vehicle
-            ++v;
-            cur = v < nv ? s_veh[v * kGenBlock + tid] : 0xffu;
-            soc_cur = v < nv ? s_soc[v * kGenBlock + tid] : 0.0;
-            req_cur = (v < nv && p.req_enabled) ? s_req[v * kGenBlock + tid] : 1.0;
-        }
+        v += (t > (int)((cur >> 8) & 0xffu)) ? 1 : 0;   // past the current departure: next vehicle
+        cur = s_veh[v * kGenBlock + tid];                // (re-)read unconditionally: no divergence
+        soc_cur = s_soc[v * kGenBlock + tid];
+        if (p.req_enabled) req_cur = s_req[v * kGenBlock + tid];
         const int ta = (int)(cur & 0xffu), dep = (int)((cur >> 8) & 0xffu);
         const uint32_t cap = (cur >> 16) & 0xffu;
         const bool occ = t >= ta && t < dep;
