@@ -602,7 +602,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     const uint32_t *__restrict__ word_t = word + tbase * (size_t)E;   // this step's timeline planes
     const double *__restrict__ aux_t = auxv + tbase * (size_t)E;
     const double *__restrict__ req_t = reqv + tbase * (size_t)E;
-    uint32_t w[CH];
+    uint32_t w[CH], auxh[CH];
     double aux[CH], run[CH], req[CH];
     auto load_state = [&](int c0) {
 #pragma unroll
@@ -613,7 +613,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                 if (PK) {   // packed device-day record: word | float32 aux << 32 (sng_layout.h)
                     const uint64_t rec = bld(reinterpret_cast<const uint64_t *>(aux_t), el8, r8);
                     w[j] = (uint32_t)rec;
-                    aux[j] = (double)__uint_as_float((uint32_t)(rec >> 32));
+                    auxh[j] = (uint32_t)(rec >> 32);   // widened where charger j is computed
                 } else {
                     w[j] = bld(word_t, el4, r4);
                     aux[j] = bld(aux_t, el8, r8);
@@ -622,6 +622,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             } else {
                 w[j] = 0u;
                 aux[j] = run[j] = 0.0;
+                auxh[j] = 0u;
             }
         }
     };
@@ -728,22 +729,24 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     if (live) {
         for (int c0 = cbeg; c0 < cend; c0 += CH) {
             if (c0 != cbeg) load_batch(c0);
-            // all LDS reads of the batch (actions, 1/cap) ahead of the LDS writes below, so they
-            // issue back to back and the chargers' arithmetic interleaves
+            // the batch's actions ahead of the LDS writes below (they issue back to back)
             float av[CH];
             double rc[CH];
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
                 av[j] = (c < cend) ? a_row[c] : 0.0f;
-                rc[j] = kRows ? s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu] : 0.0;
             }
             if (L > 1) wave_lds_fence();   // the q rows below reuse the actions tile
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
                 if (c >= cend) break;
-                const ChargerResult r = charger_step<FAST, kRows>(p, w[j], aux[j], run[j], req[j], av[j], t, rc[j]);
+                // 1/cap from the LDS table here, not ahead with the actions: it needs charger j's
+                // record, and reading every record's up front waited for all of them
+                rc[j] = kRows ? s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu] : 0.0;
+                const double aux_j = PK ? (double)__uint_as_float(auxh[j]) : aux[j];
+                const ChargerResult r = charger_step<FAST, kRows>(p, w[j], aux_j, run[j], req[j], av[j], t, rc[j]);
                 bst<kNT>(socv, el8, r.soc, (uint32_t)c * (uint32_t)E * 8u);
                 if (DIAG) {   // 'Charger power values' and the SOC[c, t] the day record holds
                     if (info.charger_power) info.charger_power[(size_t)e * n + c] = r.pw;
@@ -760,6 +763,10 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                     s_pw[le * NC + c] = r.pw;
                     s_q[le * NC + c] = r.q;
                 }
+                // chargers in order: charger j's arithmetic waits only for its own loads
+                // (vmcnt counts down charger by charger) and overlaps the later chargers' loads;
+                // left to interleave them, the scheduler hoisted work that waited for all loads
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
     }
