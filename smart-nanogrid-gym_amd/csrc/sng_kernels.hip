@@ -421,28 +421,25 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
             bst(s.bess0, el8, bess);
             bess0 = bess;
         }
+        // charge (ba > 0, battery_energy_storage_system.py:186-218) and discharge (ba < 0,
+        // :220-262) share one select-based path with one division: the two branches differ only
+        // in their constants, the over-discharge clamp and the SoC bound
         const double ba = (double)bess_action;
+        const bool chg = ba > 0.0;
+        const double pw = (ba * (chg ? p.bess_pmax_ch : p.bess_pmax_dis)) * (chg ? p.bess_eff_ch : p.bess_eff_dis);
+        const double calc = bess + (pw * p.dt) / p.bess_cap;
+        const double empty = bess * p.bess_cap;   // the over-discharge clamp's energy
+        const double dp = (calc < 0.0) ? -(p.dt_pow2 ? empty * p.rdt : empty / p.dt) : pw;
         if (ba == 0.0) {
             bpow = 0.0;
             bcalc = 0.0;
         } else if (!p.bounded) {
             fl |= SNG_FLAG_CHARGING_MODE;
-        } else if (ba > 0.0) {
-            const double avail = -rem;
-            const double cp = (ba * p.bess_pmax_ch) * p.bess_eff_ch;
-            const double calc = bess + (cp * p.dt) / p.bess_cap;
-            bcalc = cp;
-            bess = (1.0 < calc) ? 1.0 : calc;
-            bpow = cp;
-            rem = -(avail - cp);
         } else {
-            double dp = (ba * p.bess_pmax_dis) * p.bess_eff_dis;
-            const double calc = bess + (dp * p.dt) / p.bess_cap;
-            bcalc = dp;
-            if (calc < 0.0) dp = -((bess * p.bess_cap) / p.dt);
-            bess = (calc > 0.0) ? calc : 0.0;
-            bpow = dp;
-            rem = rem + dp;
+            bcalc = pw;
+            bess = chg ? ((1.0 < calc) ? 1.0 : calc) : ((calc > 0.0) ? calc : 0.0);
+            bpow = chg ? pw : dp;
+            rem = chg ? -((-rem) - pw) : rem + dp;
         }
         if (bess < p.bess_dod) {                                   // penaliser.py:104-111
             const double d = (p.bess_dod - bess) * 10;
