@@ -234,7 +234,10 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
  * flags: SNG_GRAPH_*; days > 1 needs SNG_GRAPH_RESET.
  * day_returns (device [days][num_envs] f64, may be NULL): day d's returns accumulate into row
  * d instead of info->episode_return, so a replay leaves every day's returns for one
- * collective per replay (bench.py gathers them over RCCL while the next replay runs). */
+ * collective per replay (bench.py gathers them over RCCL while the next replay runs).
+ * Without SNG_GRAPH_RESET the graph steps whatever day is loaded at launch; device-RNG days and
+ * host-RNG / injected days have different timeline encodings (sng_layout.h), so launching a
+ * steps-only graph over a day of the other kind than at capture fails with SNG_ERR_STATE. */
 #define SNG_GRAPH_RESET 1   /* start every day with a device-RNG reset */
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
                      const SngInfo *info, int flags, int32_t days, double *day_returns, SngGraph **out);

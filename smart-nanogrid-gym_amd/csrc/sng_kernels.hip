@@ -101,6 +101,31 @@ __device__ __forceinline__ double pairwise_row(const double *row, int n, double 
     return res;
 }
 
+// The same for a row of at most NC <= 16 entries: every slot is read in one batch of LDS reads
+// (slots at or past n hold stale values and are selected away), so the sequential tail costs
+// no LDS round trip per element.
+template <int NC>
+__device__ __forceinline__ double pairwise_row_c(const double *row, int n, double seq) {
+    static_assert(NC >= 1 && NC <= 16, "one 8-block plus tail, or two full blocks at 16");
+    if constexpr (NC < 8) {
+        return seq;
+    } else {
+        if (n < 8) return seq;
+        double r[NC];
+#pragma unroll
+        for (int j = 0; j < NC; ++j) r[j] = row[j];
+        if (NC == 16 && n == 16) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) r[j] += r[(j + 8) % NC];
+            return ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        }
+        double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+        for (int i = 8; i < NC; ++i) res = (i < n) ? res + r[i] : res;
+        return res;
+    }
+}
+
 __host__ __device__ constexpr int round4(int x) { return (x + 3) & ~3; }
 
 // Raw buffer access: V# = an array (or a per-step timeline plane) in SGPRs, a wave-uniform
@@ -807,8 +832,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         pen_v += pen0;
         double p_ch, p_dis;
         if (kRows) {
-            p_ch = pairwise_row(row_pos, n_pos, seq_pos);
-            p_dis = pairwise_row(row_neg, n_neg, seq_neg);
+            constexpr int W = (NC > 0 && NC <= 16) ? NC : 1;   // kRows: NC in [1, 16]
+            p_ch = pairwise_row_c<W>(row_pos, n_pos, seq_pos);
+            p_dis = pairwise_row_c<W>(row_neg, n_neg, seq_neg);
         } else if (L > 1) {
             p_ch = pairwise_row(s_pw + le * NC, n_pos, seq_pos);
             p_dis = pairwise_row(s_q + le * NC, n_neg, seq_neg);
