@@ -484,7 +484,7 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     bst<kNT>(reward, el8, -total);
     bst<kNT>(done, el1, (uint8_t)((t + 1 == p.T) ? 1 : 0));
 
-    write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio, fpv, fpr);
+    // (the observation header was written before the chargers: step_kernel)
     if (p.bess) o_row[p.obs_dim - 1] = (float)bess;
 
     if (fl) atomicOr(s.flags + e0 + lo, fl);   // rare (sticky error bits); no-return atomic, nothing waits
@@ -717,6 +717,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     float *o_row = s_obs + le * O;
     const float bess_action = p.bess ? a_row[n] : 0.0f;   // before the q rows reuse the tile
     const int k_soc = (p.pv ? 8 : 4);
+    // the observation header needs only the PV ratio and this step's constants: written here,
+    // while the chargers' loads are still in flight, instead of at the end of the env tail
+    if (live && leader) write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio, fpv, fpr);
     PairwiseSum pos, neg;
     double seq_pos = 0.0, seq_neg = 0.0;
     int n_pos = 0, n_neg = 0;
