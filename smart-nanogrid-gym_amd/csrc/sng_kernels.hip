@@ -1042,8 +1042,8 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
-    const uint32_t el4 = (uint32_t)e * 4u, el8 = (uint32_t)e * 8u;
-    const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
+    const uint32_t el8 = (uint32_t)e * 8u;
+    const uint32_t r8 = (uint32_t)c * (uint32_t)E * 8u;
     for (int t = 0; t < T; ++t) {
         v += (t > (int)((cur >> 8) & 0xffu)) ? 1 : 0;   // past the current departure: next vehicle
         cur = s_veh[v * kGenBlock + tid];                // (re-)read unconditionally: no divergence
