@@ -25,8 +25,10 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
                            int vec_io, hipStream_t stream);
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
+                           float *obs, double *ep_return, int vec_io,
                            hipStream_t stream);
 hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream);
+hipError_t launch_bump_day(const DeviceState &s, hipStream_t stream);
 int step_lanes_supported(int n, int lanes);
 }  // namespace sng
 
@@ -714,15 +716,18 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     hipStream_t st = (hipStream_t)stream;
     if (rng_mode == SNG_RNG_DEVICE) {
         if (!device_rng_ok(env)) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
+        const bool unstepped_device_day = env->p.packed && env->t == 0;
         env->p.req_stream = env->p.req_enabled;
         env->p.packed = 1;   // the generator writes packed records (sng_layout.h)
         if (env->p.req_stream) {
             int rc = ensure_req(env);
             if (rc) return rc;
         }
-        HIP_TRY(env, launch_generate(env->p, env->ds, env->seed, env->E, env->i4, env->i10, env->i1, st));
-        HIP_TRY(env, launch_profiles(env->p, env->ds, env->E, st));
-        HIP_TRY(env, launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st));
+        // a device day's first step advances the day counter (step_kernel); a second device reset
+        // with no step in between advances it here, so it still draws a new day
+        if (unstepped_device_day) HIP_TRY(env, launch_bump_day(env->ds, st));
+        HIP_TRY(env, launch_generate(env->p, env->ds, env->seed, env->E, env->i4, env->i10, env->i1, obs, nullptr,
+                                     aligned16(obs) ? 1 : 0, st));
         env->t = 0;
         env->day_finished = false;
         return SNG_OK;
@@ -999,9 +1004,7 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
         InfoPtrs ipd = ip;   // day d's returns into row d (observe0 zeroes it, every step adds)
         if (day_returns) ipd.episode_return = day_returns + (size_t)d * E;
         if (with_reset) {
-            e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, cs);
-            if (e == hipSuccess) e = launch_profiles(p, env->ds, E, cs);
-            if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ipd.episode_return, E, vec, cs);
+            e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, obs, ipd.episode_return, vec, cs);
         }
         for (int t = 0; e == hipSuccess && t < p.T; ++t)
             e = launch_step(p, env->ds, ipd, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
@@ -1027,6 +1030,8 @@ int sng_graph_launch(SngGraph *g, void *stream) {
     if (!g->with_reset && g->packed != env->p.packed)
         return fail(env, SNG_ERR_STATE, "graph captured for days of the other RNG mode: recapture it after this reset");
     HIP_TRY(env, hipSetDevice(env->device));
+    // the graph's first reset must not redraw a device day that was reset but never stepped
+    if (g->with_reset && env->p.packed && env->t == 0) HIP_TRY(env, launch_bump_day(env->ds, (hipStream_t)stream));
     HIP_TRY(env, hipGraphLaunch(g->exec, (hipStream_t)stream));
     if (g->with_reset) {
         env->p.req_stream = env->p.req_enabled;
@@ -1065,12 +1070,11 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
     std::vector<hipEvent_t> ev(2 * (size_t)T * days, nullptr);
     hipError_t e = hipSuccess;
+    if (env->p.packed && env->t == 0) e = launch_bump_day(env->ds, st);   // as in sng_reset
     for (auto &x : ev)
         if (e == hipSuccess) e = hipEventCreate(&x);
     for (int d = 0; e == hipSuccess && d < days; ++d) {
-        e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, st);
-        if (e == hipSuccess) e = launch_profiles(p, env->ds, E, st);
-        if (e == hipSuccess) e = launch_observe0(p, env->ds, obs, ip.episode_return, E, vec, st);
+        e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, obs, ip.episode_return, vec, st);
         for (int t = 0; e == hipSuccess && t < T; ++t) {
             hipEvent_t a = ev[2 * ((size_t)d * T + t)], b = ev[2 * ((size_t)d * T + t) + 1];
             e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, st, a, b);

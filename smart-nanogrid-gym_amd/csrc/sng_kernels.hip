@@ -852,6 +852,9 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     wave_lds_fence();
     SNG_STAMP(2);
     copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
+    // a device-RNG day's first step advances the day counter its reset read (generate_kernel);
+    // nothing in this launch reads it (done last: at the top it perturbed the prologue's schedule)
+    if (PK && t == 0 && blockIdx.x == 0 && threadIdx.x == 0) *s.episode += 1;
     SNG_STAMP(3);
 }
 
@@ -974,14 +977,107 @@ __host__ __device__ constexpr size_t generate_lds_bytes(bool with_req) {
     return (size_t)kDayVehicles * kGenBlock * (sizeof(uint32_t) + sizeof(double) + (with_req ? sizeof(double) : 0));
 }
 
+// One vehicle's draws (charging_station.py:257-279), in stream order: the geometric wait from
+// tfree to the arrival, arrival SoC, capacity + departure, requested SoC.  Phase 1 below and the
+// t = 0 observation blocks share it, so both see the same first vehicle.
+struct VehicleDraw {
+    int ta, dep;
+    uint32_t cap;
+    double soc;
+    uint32_t req_draw;
+};
+__device__ __forceinline__ VehicleDraw draw_vehicle(const Params &p, HashStream &rng, int tfree, int i4, int i10,
+                                                    int i1) {
+    VehicleDraw d;
+    const float u = ((float)(rng.next() >> 8) + 1.0f) * 0x1.0p-24f;   // (0, 1]
+    d.ta = tfree + (int)(__log2f(u) * kInvLog2Q);                       // floor: the product is >= 0
+    // uniform(0.1, 0.9), drawn as a float32 value (the packed record holds it exactly)
+    d.soc = (double)(float)(0.1 + (0.9 - 0.1) * u32_unit(rng.next()));
+    // capacity and departure from one draw: cap = floor(y * 105 / 2^32); the low word of
+    // y * 105 (a bijection of y, uniform given cap) drives the departure
+    const uint32_t y = rng.next();
+    d.cap = p.diff_caps ? (uint32_t)(15 + below(y, 105)) : 40u;   // randint(15, 120)
+    const uint32_t yd = p.diff_caps ? y * 105u : y;
+    const int hi_c = d.ta + i10, hi_d = p.T + i1;
+    const int high = hi_c < hi_d ? hi_c : hi_d;
+    const int low = d.ta + i4;
+    d.dep = (low >= high) ? low : low + below(yd, high - low);
+    d.req_draw = p.req_enabled ? rng.next() : 0u;
+    return d;
+}
+
+__device__ __forceinline__ double pv_ratio_draw(uint64_t seed, uint64_t ge, uint64_t day) {
+    HashStream r2{stream_key(seed, ge, 0x7a710000u, day), 0u};   // the PV-ratio domain
+    return (double)below(r2.next(), 181) / 100;                   // random.randint(0, 180) / 100
+}
+
+// The t = 0 observation of a device-RNG day, computed from the streams rather than read back from
+// the timeline, so it runs as extra blocks of the generator's grid with no dependency on the
+// timeline blocks (SmartNanogridEnv.reset -> __get_observations, smart_nanogrid_environment.py:
+// 358-360): each charger's first vehicle, if it arrives at t = 0, gives SOC[c, 0] and the
+// departure entry; the PV ratio, the day's profile factors, the header and the BESS entry; the
+// running SoC is seeded and the day return zeroed.  Thread = env; rows leave through LDS.
+__device__ __forceinline__ void observe_day0(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4,
+                                             int i10, int i1, uint64_t day, float *__restrict__ obs,
+                                             double *__restrict__ ep_return, int vec_io, float *lds) {
+    const int n = p.n, O = p.obs_dim;
+    const int tid = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * kGenBlock;
+    const int nblk = (int)((E - e0) < kGenBlock ? (E - e0) : kGenBlock);
+    const int64_t e = e0 + tid;
+    float *o_row = lds + tid * O;
+    if (tid < nblk) {
+        const uint64_t ge = (uint64_t)(e + p.env_offset);
+        const double ratio = pv_ratio_draw(seed, ge, day);
+        s.ratio[e] = ratio;
+        s.pen0[e] = 0.0;
+        double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
+        if (p.noise) {   // the day's profile factors prof[2][T + 3][E] (profile_kernel's)
+            const uint64_t env_seed = p.seed + (uint64_t)p.env_offset + (uint64_t)e;
+            const size_t pl = (size_t)(p.T + 3) * E;
+            for (int k = 0; k < p.T + 3; ++k) {
+                const double a = p.pv_noise != 0.0 ? profile_factor(env_seed, kDomainPV, day, k, p.pv_noise) : 1.0;
+                const double b =
+                    p.price_noise != 0.0 ? profile_factor(env_seed, kDomainPrice, day, k, p.price_noise) : 1.0;
+                s.prof[(size_t)k * E + e] = a;
+                s.prof[pl + (size_t)k * E + e] = b;
+                if (k < 4) {
+                    fpv[k] = a;
+                    fpr[k] = b;
+                }
+            }
+        }
+        write_obs_header(o_row, p, s.tables->irr_norm, s.tables->price_norm, ratio, fpv, fpr);
+        const int k = p.pv ? 8 : 4;
+        const uint32_t el8 = (uint32_t)e * 8u;
+        for (int c = 0; c < n; ++c) {
+            HashStream rng{stream_key(seed, ge, (uint32_t)c, day), 0u};
+            const VehicleDraw d = draw_vehicle(p, rng, 0, i4, i10, i1);
+            const bool occ0 = d.ta == 0;   // t = 0 < T always, and dep >= 4/dt > 0
+            const double soc0 = occ0 ? d.soc : 0.0;
+            bst<kNT>(s.soc, el8, soc0, (uint32_t)c * (uint32_t)E * 8u);
+            o_row[k + c] = (float)soc0;
+            o_row[k + n + c] = departure_obs(pack_word(occ0, occ0, false, 0u, occ0 ? (uint32_t)d.dep : 0u));
+        }
+        if (p.bess) o_row[O - 1] = (float)s.bess[e];
+        if (ep_return) ep_return[e] = 0.0;
+    }
+    __syncthreads();
+    copy_out<kGenBlock>(obs + e0 * O, lds, nblk * O, vec_io != 0, tid);
+}
+
 // Two phases per (env, charger):
 //  1. the day's vehicles: the waiting time to the next arrival is the number of failed
 //     Bernoulli(0.4) trials before the first success (geometric, one draw via -log2(u)/-log2(0.6)),
 //     then arrival SoC, capacity and departure -- a few draws per vehicle instead of one per free
 //     step, without the per-step divergent arrival branch;
 //  2. the dense timeline, step by step, from the vehicle list kept in LDS.
+// Grid (E / 256, N + 1): blocks y < N write charger y's timeline, blocks y = N the t = 0
+// observation (observe_day0).  The day counter is read here and advanced by the day's first step
+// (step_kernel, t = 0), so no block of this grid waits on another.
 __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
-                                                             int i4, int i10, int i1) {
+                                                             int i4, int i10, int i1, float *__restrict__ obs,
+                                                             double *__restrict__ ep_return, int vec_io) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     uint32_t *s_veh = reinterpret_cast<uint32_t *>(lds);                        // [V][BLOCK] arr | dep<<8 | cap<<16
     double *s_soc = reinterpret_cast<double *>(s_veh + kDayVehicles * kGenBlock);   // [V][BLOCK]
@@ -989,8 +1085,12 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     const int tid = threadIdx.x;
     const int64_t e = (int64_t)blockIdx.x * kGenBlock + tid;
     const int c = blockIdx.y;
-    if (e >= E) return;
     const uint64_t day = *s.episode;
+    if (c == p.n) {
+        observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds);
+        return;
+    }
+    if (e >= E) return;
     const uint64_t ge = (uint64_t)(e + p.env_offset);   // global env id
     HashStream rng{stream_key(seed, ge, (uint32_t)c, day), 0u};
     const int T = p.T, n = p.n;
@@ -999,28 +1099,16 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     int tfree = 0, nv = 0;
     for (int v = 0; v < kDayVehicles - 1; ++v) {   // the last slot holds the sentinel
         if (tfree >= T) break;
-        const float u = ((float)(rng.next() >> 8) + 1.0f) * 0x1.0p-24f;   // (0, 1]
-        const int ta = tfree + (int)(__log2f(u) * kInvLog2Q);             // floor: the product is >= 0
-        if (ta >= T) break;
-        // uniform(0.1, 0.9), drawn as a float32 value (the packed record holds it exactly)
-        const double soc_arr = (double)(float)(0.1 + (0.9 - 0.1) * u32_unit(rng.next()));
-        // capacity and departure from one draw: cap = floor(y * 105 / 2^32); the low word of
-        // y * 105 (a bijection of y, uniform given cap) drives the departure
-        const uint32_t y = rng.next();
-        const uint32_t cap = p.diff_caps ? (uint32_t)(15 + below(y, 105)) : 40u;   // randint(15, 120)
-        const uint32_t yd = p.diff_caps ? y * 105u : y;
-        const int hi_c = ta + i10, hi_d = T + i1;
-        const int high = hi_c < hi_d ? hi_c : hi_d;
-        const int low = ta + i4;
-        const int dep = (low >= high) ? low : low + below(yd, high - low);
-        s_veh[v * kGenBlock + tid] = (uint32_t)ta | ((uint32_t)dep << 8) | (cap << 16);
-        s_soc[v * kGenBlock + tid] = soc_arr;
+        const VehicleDraw d = draw_vehicle(p, rng, tfree, i4, i10, i1);
+        if (d.ta >= T) break;
+        s_veh[v * kGenBlock + tid] = (uint32_t)d.ta | ((uint32_t)d.dep << 8) | (d.cap << 16);
+        s_soc[v * kGenBlock + tid] = d.soc;
         if (p.req_enabled) {
-            const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
-            s_req[v * kGenBlock + tid] = lo + (1.0 - lo) * u32_unit(rng.next());
+            const double lo = d.soc <= 0.9 ? d.soc + 0.1 : 1.0;
+            s_req[v * kGenBlock + tid] = lo + (1.0 - lo) * u32_unit(d.req_draw);
         }
         nv = v + 1;
-        tfree = dep + 1;   // the departure step stays empty (charging_station.py:247-255)
+        tfree = d.dep + 1;   // the departure step stays empty (charging_station.py:247-255)
     }
 
     // slot nv: a sentinel that never arrives (arrival = departure = 255), so phase 2 walks the
@@ -1069,11 +1157,6 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         prev_rem = rem;
     }
     if (p.req_stream) bst(s.req, el8, prev_occ ? req_cur : 0.0, r8);
-    if (c == 0) {
-        HashStream r2{stream_key(seed, ge, 0x7a710000u, day), 0u};            // the PV-ratio domain
-        s.ratio[e] = (double)below(r2.next(), 181) / 100;   // random.randint(0, 180) / 100
-        s.pen0[e] = 0.0;
-    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1172,11 +1255,32 @@ hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, do
     return hipGetLastError();
 }
 
+hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
+                           int vec_io, hipStream_t stream);
+hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream);
+
+// A whole device-RNG reset.  The t = 0 observation runs as extra blocks of the generator's grid
+// while its [256][obs_dim] LDS tile stays small next to the vehicle lists (N <= 16: at most 42 KB,
+// a few generator workgroups per CU still fit); wider stations keep profile_kernel and
+// observe0_kernel as separate launches behind the generator.
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
-                           hipStream_t stream) {
-    const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)p.n), block(kGenBlock);
-    hipLaunchKernelGGL(generate_kernel, grid, block, generate_lds_bytes(p.req_enabled != 0), stream, p, s, seed, E, i4,
-                       i10, i1);
+                           float *obs, double *ep_return, int vec_io, hipStream_t stream) {
+    const size_t veh = generate_lds_bytes(p.req_enabled != 0), tile = (size_t)round4(kGenBlock * p.obs_dim) * 4;
+    const bool fused = tile <= 48 * 1024;
+    const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(p.n + (fused ? 1 : 0))), block(kGenBlock);
+    hipLaunchKernelGGL(generate_kernel, grid, block, (fused && tile > veh) ? tile : veh, stream, p, s, seed, E, i4, i10,
+                       i1, obs, ep_return, vec_io);
+    if (fused) return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = launch_profiles(p, s, E, stream);
+    if (e == hipSuccess) e = launch_observe0(p, s, obs, ep_return, E, vec_io, stream);
+    return e;
+}
+
+__global__ void bump_day_kernel(DeviceState s) { *s.episode += 1; }
+
+hipError_t launch_bump_day(const DeviceState &s, hipStream_t stream) {
+    hipLaunchKernelGGL(bump_day_kernel, dim3(1), dim3(1), 0, stream, s);
     return hipGetLastError();
 }
 

@@ -260,6 +260,39 @@ def test_episode_graph_matches_eager_device_rng():
     b.close()
 
 
+def test_every_device_reset_draws_a_new_day():
+    """The device day counter is read by the reset and advanced by the day's first step; resets
+    with no step in between (eager, or an eager reset followed by a graph replay) must still
+    draw new days, and the same sequence of calls must give the same days."""
+    E, N = 4096, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse")
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+
+    def run(v):
+        days = [v.reset_tensors().clone(), v.reset_tensors().clone()]   # twice, no step between
+        for t in range(24):
+            v.step_tensors(acts[t])
+        days.append(v.reset_tensors().clone())
+        g = EpisodeGraph(v, acts)   # an eager reset, then a graph whose reset must draw a new day
+        g.launch()
+        torch.cuda.synchronize()
+        g.close()
+        days.append(v.reset_tensors().clone())
+        return days
+
+    a = SmartNanogridVecEnv(E, seed=21, rng="device", **kw)
+    b = SmartNanogridVecEnv(E, seed=21, rng="device", **kw)
+    da, db = run(a), run(b)
+    for x, y in zip(da, db):
+        assert torch.equal(x, y)
+    for i in range(len(da)):
+        for j in range(i + 1, len(da)):
+            assert not torch.equal(da[i], da[j]), (i, j)
+    a.close()
+    b.close()
+
+
 def test_step_graph_follows_the_day_encoding():
     """A steps-only graph (the T steps of a day, no reset) replays the day that is loaded:
     device-RNG days are packed 8 B records, host-RNG days word + float64 planes (sng_layout.h).
