@@ -56,8 +56,9 @@ typedef enum SngRngMode {
      * reference's reset()/step() sequence (charging_station.py:200-279,
      * smart_nanogrid_environment.py:190,358).  Generated on the host CPU threads. */
     SNG_RNG_REFERENCE = 0,
-    /* Counter-based hash streams on the GPU: same distributions, different draws.
-     * Fully device-resident; graph-capturable. */
+    /* Counter-based hash streams on the GPU: same distributions, different draws (the arrival
+     * SoC is drawn as a float32 value).  Fully device-resident; graph-capturable.  Each device
+     * reset draws a new day of the handle's day counter, which the day's first step advances. */
     SNG_RNG_DEVICE = 1
 } SngRngMode;
 
