@@ -1,3 +1,10 @@
+# Generator / step diagnostics on the GPU box (gpurun -- 'bash tools/gpu_diag.sh'):
+#   1. kernel stats of the default build and of a build without hashing, for the generator's floor
+#      (hipcc ... -DSNG_GEN_CHEAP -shared -o smart-nanogrid-gym_amd/lib/libsng_gencheap.so
+#       sng_kernels.hip sng_api.cpp, in smart-nanogrid-gym_amd/csrc, beforehand);
+#   2. one SQ counter pass (8 SQ counters: the per-pass limit) -> tools/sq_summary.py;
+#   3. the step kernel at 2 and 4 lanes per env.
+# Every GPU step has its own time limit and the script stops at the first failure.
 set -u
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp
