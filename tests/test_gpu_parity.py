@@ -107,7 +107,8 @@ def _oracle_batch(kw, seed, idx):
 
 @pytest.mark.parametrize("E,N,mode,lanes", [(4096, 10, "sparse", 1), (4096, 10, "sparse", 2), (4096, 10, "dense", 4),
                                             (1024, 50, "sparse", 0), (1024, 50, "dense", 4), (1000, 4, "on_departure", 2),
-                                            (333, 1, "sparse", 0), (777, 7, "dense", 0), (300, 16, "sparse", 4)])
+                                            (333, 1, "sparse", 0), (777, 7, "dense", 0), (300, 16, "sparse", 4),
+                                            (512, 33, "dense", 0), (256, 128, "sparse", 0)])
 def test_batched_reference_rng_vs_oracle_bit_exact(E, N, mode, lanes):
     """Config 2 (4,096 envs x 10 chargers x 24 steps): every env against the oracle seeded base+i,
     two consecutive days, random actions with 20 % exact zeros."""

@@ -137,10 +137,11 @@ def test_recorder_matches_oracle_reference_rng(name):
     venv.close()
 
 
-@pytest.mark.parametrize("req", [False, True])
-def test_device_day_decode_round_trip(req):
-    """Device-RNG days decoded to the reference layout and re-injected step bit for bit like the original."""
-    kw = dict(number_of_chargers=10, time_interval="1h", charging_mode="bounded",
+@pytest.mark.parametrize("N,req", [(10, False), (10, True), (33, True), (128, False)])
+def test_device_day_decode_round_trip(N, req):
+    """Device-RNG days decoded to the reference layout and re-injected step bit for bit like the original.
+    N = 33 and 128 (the maximum) take the generic step kernel and the separate t = 0 observation launch."""
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
               vehicle_uncharged_penalty_mode="dense" if req else "sparse", enable_requested_state_of_charge=req)
     E = 256
     a_dev = SmartNanogridVecEnv(E, seed=99, rng="device", **kw)
