@@ -137,20 +137,25 @@ def test_recorder_matches_oracle_reference_rng(name):
     venv.close()
 
 
-@pytest.mark.parametrize("N,req", [(10, False), (10, True), (33, True), (128, False)])
-def test_device_day_decode_round_trip(N, req):
+@pytest.mark.parametrize("N,req,dt", [(10, False, "1h"), (10, True, "1h"), (33, True, "1h"), (128, False, "1h"),
+                                      (10, True, "30min"), (16, False, "20min"), (4, True, "2h")])
+def test_device_day_decode_round_trip(N, req, dt):
     """Device-RNG days decoded to the reference layout and re-injected step bit for bit like the original.
-    N = 33 and 128 (the maximum) take the generic step kernel and the separate t = 0 observation launch."""
-    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+    N = 33 and 128 (the maximum) take the generic step kernel and the separate t = 0 observation launch;
+    20 min (dt = 1/3, not a power of two) takes the division path of the step."""
+    kw = dict(number_of_chargers=N, time_interval=dt, charging_mode="bounded",
               vehicle_uncharged_penalty_mode="dense" if req else "sparse", enable_requested_state_of_charge=req)
+    if dt.endswith("min"):
+        kw["extended_day"] = True   # sub-hour days need the build-defined extension (section 5.4)
     E = 256
     a_dev = SmartNanogridVecEnv(E, seed=99, rng="device", **kw)
     b_inj = SmartNanogridVecEnv(E, seed=0, **kw)
     obs_a = a_dev.reset_tensors().cpu().numpy().copy()
     ivs, ratios = zip(*[a_dev.get_scenario(i) for i in range(E)])
-    for iv in ivs:   # the device generator's process: every vehicle stays >= 4 steps
+    min_stay = a_dev.timesteps // 6   # the device generator's process: every vehicle stays >= 4 h
+    for iv in ivs:
         for arr, dep in zip(iv["Arrivals"], iv["Departures"]):
-            assert all(d - a >= 4 for a, d in zip(arr, dep))
+            assert all(d - a >= min_stay for a, d in zip(arr, dep))
     b_inj.set_battery_state_of_charge(a_dev.battery_state_of_charge())
     obs_b = b_inj.reset_from_initial_values(list(ivs), np.array(ratios), restore_requested_soc=True)
     np.testing.assert_array_equal(obs_a, obs_b)
