@@ -11,14 +11,22 @@ action Box, 20 % exact zeros), pre-generated on the device outside the timed reg
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 Rank 0 prints one JSON line.  `roofline` describes the dominant kernel (the fused step):
-achieved = algorithmic bytes per launch / mean launch time from HIP start/stop events attached
-to every step-kernel dispatch (eager days right after the timed region); `traffic` comes from
-the committed rocprofv3 PMC summary (profiles/), null if absent.  `cpu_baseline` is the C
-oracle (a scalar port of the reference step/reset) on one host core, bounded sample.
+achieved = SURVEY.md 8(d)'s algorithmic bytes per env-step, B(N) = 40 N + 65 (465 B at N = 10),
+x the envs of one launch / the mean launch time from HIP start/stop events attached to every
+step-kernel dispatch (eager days right after the timed region, on the stream the kernel runs on).
+`frac_rocprof` is the same bytes over the average duration of that kernel in the committed
+rocprofv3 --kernel-trace --stats summary (profiles/), when one exists for this kernel; `traffic` is
+the HBM bytes per launch from the committed PMC passes, null if absent.  `cpu_baseline` is the C
+restatement of the reference's step()/reset() (oracle/, kind "port", label "restatement") run as one
+process per host core of sched_getaffinity (capped by OMP_NUM_THREADS), measured before the GPU is
+touched, with the reference's own Python step() range from SURVEY.md section 6 beside it.
 """
 import argparse
+import glob
 import json
+import multiprocessing
 import os
+import re
 import sys
 import time
 
@@ -33,35 +41,78 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 METRIC = "env-steps/sec (whole node) at N=65,536 envs × 10 chargers, 24-step day"
 
 
+def survey_bytes(n):
+    """SURVEY.md 8(d) canonical algorithmic bytes per env-step (b-pv): actions 4(N+1) + obs 4(2N+9) +
+    reward 8 + done 1 + EV SoC r/w 16N + BESS r/w 16 + scenario 12N = 40 N + 65."""
+    return 40 * n + 65
+
+
 def step_kernel_bytes(n, noise=False):
-    """Algorithmic bytes one env moves in one fused step of a device-RNG day (b-pv, no
-    requested-SoC stream): actions 4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N
-    + packed charger-step record 8N (scenario word + float32 static SoC) + BESS r/w 16 + PV ratio 8
-    + day-return r/w 16 = 36N + 89 (+ 64 for the PV / price profile factors of t..t+3 with
-    stochastic profiles).  Host-RNG days read the word and a float64 static SoC instead: 40N + 89."""
+    """What this layout moves per env-step of a device-RNG day (b-pv, no requested-SoC stream): actions
+    4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N + packed charger-step record 8N (scenario
+    word + float32 static SoC) + BESS r/w 16 + PV ratio 8 + day-return r/w 16 = 36N + 89 (+ 64 for the
+    PV / price profile factors of t..t+3 with stochastic profiles).  Host-RNG days read the word and a
+    float64 static SoC instead: 40N + 89."""
     return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 8 * n + 16 + 8 + 16 + (64 if noise else 0)
 
 
-def cpu_baseline(kw, budget_s):
+def _cpu_worker(job):
+    """One host process of the CPU baseline: whole days (reset + T steps) of independent oracle envs."""
+    kw, budget_s, wid = job
     import oracle as O
     cfg = O.OracleConfig(**kw)
-    chargers = cfg.N
-    A = cfg.act_dim
     batch = 256
-    rng = np.random.default_rng(0)
-    acts = rng.uniform(0, 1, (cfg.T, batch, A)).astype(np.float32)
+    rng = np.random.default_rng(wid)
+    acts = rng.uniform(0, 1, (cfg.T, batch, cfg.act_dim)).astype(np.float32)
     acts[..., -1] = acts[..., -1] * 2 - 1
     acts[rng.random(acts.shape) < 0.2] = 0
     envs = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < budget_s:
-        O.run_batch(cfg, batch, envs, 1, acts)
+        O.run_batch(cfg, batch, 10_000_000 * wid + envs, 1, acts)
         envs += batch
-    dt = time.perf_counter() - t0
-    return {"value": envs * cfg.T / dt, "unit": "env-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{envs} envs x 1 day (reset + {cfg.T} steps each), b-pv N={chargers} sparse "
-                      f"{kw.get('time_interval', '1h')}, "
-                      f"C oracle (scalar restatement of the reference) on 1 host thread, {dt:.1f} s"}
+    return envs * cfg.T, time.perf_counter() - t0
+
+
+def cpu_baseline(kw, budget_s):
+    """The restatement on every host core this process may use (sched_getaffinity, capped by
+    OMP_NUM_THREADS / SNG_CPU_BASELINE_PROCS: a GPU box shows the whole machine but gives a process a
+    share), one process per core, forked before the GPU is initialised."""
+    affinity = len(os.sched_getaffinity(0))
+    cap = os.environ.get("SNG_CPU_BASELINE_PROCS") or os.environ.get("OMP_NUM_THREADS")
+    procs = max(1, min(affinity, int(cap))) if cap else affinity
+    import oracle as O
+    O.lib()   # build / load once in the parent: the forked workers inherit it
+    with multiprocessing.get_context("fork").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(kw, budget_s, w) for w in range(procs)])
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    per = [r[0] / r[1] for r in res]
+    T = O.OracleConfig(**kw).T
+    return {"value": steps / wall, "unit": "env-steps/s", "cores": procs, "kind": "port", "label": "restatement",
+            "per_process": float(np.mean(per)),
+            "sample": f"{steps // T} envs x 1 day (reset + {T} steps each), b-pv N={kw['number_of_chargers']} sparse "
+                      f"{kw.get('time_interval', '1h')}; C restatement of the reference (oracle/), {procs} processes "
+                      f"(sched_getaffinity {affinity} CPUs, cap {cap or 'none'}), {wall:.1f} s",
+            "reference_python": {"value": [4700, 8200], "unit": "env-steps/s per core",
+                                 "source": "SURVEY.md section 6: the reference's own step()+reset(), N=10, JSON I/O "
+                                           "stubbed, in the build container (the reference does not exist on the "
+                                           "GPU box)"}}
+
+
+def rocprof_average_us(kernel, extended):
+    """Average duration (us) of `kernel` in the newest committed rocprofv3 --stats summary of this
+    configuration (profiles/rNN_kernel_stats[_config5].csv), with the file it came from."""
+    pat = "r*_kernel_stats_config5.csv" if extended else "r*_kernel_stats.csv"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)),
+                   key=lambda f: int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)))
+    for path in reversed(files):
+        with open(path) as fp:
+            for line in fp:
+                if line.startswith(f'"{kernel}('):
+                    cols = line.rsplit('",', 1)[1].split(",")
+                    return float(cols[2]) / 1e3, os.path.relpath(path, ROOT)
+    return None, None
 
 
 def load_pmc_traffic(n_envs, chargers, kernel):
@@ -101,6 +152,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    E, N = args.envs, args.chargers
+    kw = dict(number_of_chargers=N, time_interval=args.time_interval, charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
+              battery_system_available_in_model=True)
+    noise = args.pv_noise > 0 or args.price_noise > 0
+    if args.extended_day or noise:
+        kw.update(extended_day=args.extended_day, pv_noise=args.pv_noise, price_noise=args.price_noise)
+    # the CPU baseline is a rank-0, single-GPU report, measured before the GPU is initialised (forked
+    # workers, host cores otherwise idle)
+    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(kw, args.cpu_budget)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -112,13 +173,6 @@ def main():
     from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv
     from smart_nanogrid_gym.parallel import DayReturnExchange, max_over_ranks, shard_envs
 
-    E, N = args.envs, args.chargers
-    kw = dict(number_of_chargers=N, time_interval=args.time_interval, charging_mode="bounded",
-              vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
-              battery_system_available_in_model=True)
-    noise = args.pv_noise > 0 or args.price_noise > 0
-    if args.extended_day or noise:
-        kw.update(extended_day=args.extended_day, pv_noise=args.pv_noise, price_noise=args.price_noise)
     offset, _ = shard_envs(world * E, world, rank)   # weak scaling: E envs per GPU, global ids
     venv = SmartNanogridVecEnv(E, seed=args.seed, device=local, rng="device", env_offset=offset,
                                step_lanes_per_env=args.lanes, **kw)
@@ -131,6 +185,8 @@ def main():
     acts = acts.contiguous()
     # the bench's info: only the per-env day return (for the all-gather), no diagnostics
     venv._info.flags = None
+    venv.reset_tensors(rng="device")
+    kernel = venv.step_kernel_name()   # the instantiation the graphs below launch (device-RNG days)
     # days per graph replay (the same at every N, so per-GPU work is identical)
     D = max(1, args.graph_days)
     while args.steps % D:
@@ -191,15 +247,16 @@ def main():
         env_steps = world * E * T * args.steps
         value = env_steps / elapsed
         launch_s = float(np.mean(kernel_ms)) / 1e3
-        bpl = step_kernel_bytes(N, noise) * E
+        bpl = survey_bytes(N) * E
         achieved = bpl / launch_s / 1e9
-        kernel = f"void sng::step_kernel<{N}, {venv.step_lanes}, false, true, true>"
+        rp_us, rp_file = rocprof_average_us(kernel, args.extended_day or noise)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N, kernel),
-                "kernel": kernel, "bytes_per_launch": bpl,
-                "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src}
-        # the CPU baseline is a rank-0, single-GPU report (it would only delay the other ranks' exit)
-        cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(kw, args.cpu_budget)
+                "kernel": kernel, "bytes_model": f"SURVEY.md 8(d) B(N) = 40N+65 = {survey_bytes(N)} B per env-step",
+                "bytes_per_launch": bpl, "layout_bytes_per_launch": step_kernel_bytes(N, noise) * E,
+                "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src,
+                "rocprof_avg_us": rp_us, "rocprof_file": rp_file,
+                "frac_rocprof": None if rp_us is None else round(bpl / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
         headline = (N == 10 and T == 24 and not noise)
         metric = METRIC if headline else f"env-steps/sec (whole node) at N={E:,} envs × {N} chargers, {T}-step day"
         desc = f"b-pv bounded sparse {args.time_interval}" + (

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 6
+#define SNG_ABI_VERSION 7
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -54,7 +54,7 @@ typedef enum SngRngMode {
     /* Host MT19937 streams identical to the reference's global RNGs: environment i
      * reproduces `np.random.seed(seed + i); random.seed(seed + i)` followed by the
      * reference's reset()/step() sequence (charging_station.py:200-279,
-     * smart_nanogrid_environment.py:190,358).  Generated on the host CPU threads. */
+     * smart_nanogrid_environment.py:181,349).  Generated on the host CPU threads. */
     SNG_RNG_REFERENCE = 0,
     /* Counter-based hash streams on the GPU: same distributions, different draws (the arrival
      * SoC is drawn as a float32 value).  Fully device-resident; graph-capturable.  Each device
@@ -64,18 +64,18 @@ typedef enum SngRngMode {
 
 /* Per-env flag bits reported by sng_read_errors / SngInfo.flags. */
 #define SNG_FLAG_NEGATIVE_DEMAND  0x1u  /* ValueError, central_management_system.py:158-159 */
-#define SNG_FLAG_CHARGING_MODE    0x2u  /* ValueError, charger.py:88/138, battery_energy_storage_system.py:230/262 */
+#define SNG_FLAG_CHARGING_MODE    0x2u  /* ValueError, charger.py:88/138, battery_energy_storage_system.py:74/106 */
 #define SNG_FLAG_BESS_SOC_ABOVE_1 0x4u  /* ValueError, penaliser.py:110-111 */
 #define SNG_FLAG_V2X_BREAKPOINT   0x8u  /* breakpoint(), central_management_system.py:160-165 (not an error) */
 
-/* Constructor keyword arguments of SmartNanogridEnv (smart_nanogrid_environment.py:41-43)
+/* Constructor keyword arguments of SmartNanogridEnv (smart_nanogrid_environment.py:32-34)
  * plus the module constants the reference hard-codes, with the reference's values as
  * defaults (sng_config_defaults). */
 typedef struct SngConfig {
     int32_t abi_version;                     /* = SNG_ABI_VERSION */
     int32_t number_of_chargers;              /* N (1..128) */
-    double time_interval_hours;              /* set_time_interval(), :134-147 ('1h' -> 1.0) */
-    int32_t price_model;                     /* accountant.py:245-288, 0..4 */
+    double time_interval_hours;              /* set_time_interval(), :125-138 ('1h' -> 1.0) */
+    int32_t price_model;                     /* accountant.py:58-101, 0..4 */
     int32_t pv_system_available;             /* pv_system_available_in_model */
     int32_t battery_system_available;        /* battery_system_available_in_model */
     int32_t vehicle_to_everything;           /* vehicle_to_everything */
@@ -84,9 +84,9 @@ typedef struct SngConfig {
     int32_t charging_mode_bounded;           /* charging_mode == 'bounded' */
     int32_t penalty_mode;                    /* SngPenaltyMode */
     int32_t numpy_legacy_promotion;          /* 1: NumPy<2 float64 EV power (the recorded KATs) */
-    double grid_cost_weight;                 /* accountant.py:222 -> 0.75 */
+    double grid_cost_weight;                 /* accountant.py:35 -> 0.75 */
     double battery_penalty_weight;           /* penaliser.py:181 -> 0.8 */
-    double selling_price_coefficient;        /* accountant.py:193 -> 0.8 */
+    double selling_price_coefficient;        /* accountant.py:6 -> 0.8 */
     /* BESS, central_management_system.py:35 */
     double bess_capacity_kwh;                /* 80 */
     double bess_initial_soc;                 /* 0.5 */
@@ -115,8 +115,8 @@ typedef struct SngConfig {
 } SngConfig;
 
 typedef struct SngDims {
-    int32_t obs_dim;        /* smart_nanogrid_environment.py:99-105 */
-    int32_t act_dim;        /* :110-127 */
+    int32_t obs_dim;        /* smart_nanogrid_environment.py:90-96 */
+    int32_t act_dim;        /* :101-118 */
     int32_t timesteps;      /* 24 / dt */
     int32_t number_of_chargers;
     int64_t num_envs;
@@ -145,7 +145,7 @@ typedef struct SngInfo {
     double *episode_return;              /* accumulated: += reward (zeroed by every reset) */
     /* per charger, [num_envs][N] (row-major, env-major); NULL = not written */
     double *charger_power;               /* 'Charger power values' (charging_station.py:282-299) */
-    double *vehicle_soc;                 /* SOC[c, t] after the step (charger.py:36-53/:86/:133) */
+    double *vehicle_soc;                 /* SOC[c, t] after the step (charger.py:37-56/:86/:136) */
 } SngInfo;
 
 /* A scenario in the reference's own layout (ChargingStation after
@@ -171,9 +171,9 @@ int32_t sng_abi_version(void);
 /* Fill `cfg` with the reference's defaults (N=8, '1h', b-pv, bounded, sparse). */
 void sng_config_defaults(SngConfig *cfg);
 
-/* SmartNanogridEnv.__init__ (smart_nanogrid_environment.py:41-129) for num_envs
+/* SmartNanogridEnv.__init__ (smart_nanogrid_environment.py:32-120) for num_envs
  * independent environments on HIP device `device`.  Builds the PV/price tables
- * (pv_system_manager.py:10-91, accountant.py:235-288), allocates device state.
+ * (pv_system_manager.py:10-91, accountant.py:48-101), allocates device state.
  * The BESS starts at bess_initial_soc and, as in the reference, is NOT reset by
  * sng_reset (central_management_system.py:93-94). */
 int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed, SngEnv **out);
@@ -188,42 +188,79 @@ int sng_get_timestep(const SngEnv *env);
  * single-GPU run bit for bit.  Call before reset. */
 int sng_set_env_offset(SngEnv *env, int64_t offset);
 
-/* SmartNanogridEnv.reset() (smart_nanogrid_environment.py:320-360): new day for every
- * env, timestep 0, writes the t=0 observation into obs[num_envs][obs_dim]. */
+/* SmartNanogridEnv.reset() (smart_nanogrid_environment.py:311-351) with generate_new_initial_values=True:
+ * a new day for every env (charging_station.py:152-186), timestep 0, the t=0 observation into
+ * obs[num_envs][obs_dim].  SNG_RNG_REFERENCE builds the days on host threads (the CPUs of
+ * sched_getaffinity, capped by SNG_HOST_THREADS / OMP_NUM_THREADS) and uploads each chunk of envs
+ * while the next is built. */
 int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream);
 
-/* reset(generate_new_initial_values=False) (:362-366, charging_station.py:119-136):
- * start a day from a given scenario (host memory, reference layout). */
+/* reset(generate_new_initial_values=False) (smart_nanogrid_environment.py:347-357): replays the day this
+ * handle last generated with sng_reset, as ChargingStation.load_initial_values (charging_station.py:
+ * 119-136) re-reads the initial_values.json the generation wrote (:185-186): arrivals, departures, SoC,
+ * occupancy and capacities as generated, Requested_SOC left at the 0 clear_initialisation_variables
+ * (:138-150) wrote (so no vehicle penalty), a new PV ratio (:349 -- reference RNG: each env's Python
+ * stream, after the owed day-end draw; device RNG: a replay stream), BESS carried over.
+ * SNG_ERR_STATE if nothing was generated yet or an injected day (sng_reset_from_scenario) replaced it. */
+int sng_reset_replay(SngEnv *env, float *obs, void *stream);
+
+/* Start a day from given days in the reference's layout (host memory): the recorded KAT days, or
+ * days exported with sng_get_scenario.  scenario->pv_ratio may be NULL: each env then draws its ratio
+ * from its Python stream (smart_nanogrid_environment.py:349) as a reset does; the day-end draw the
+ * last step owes (:181) is consumed either way once the streams exist. */
 int sng_reset_from_scenario(SngEnv *env, const SngScenario *scenario, float *obs, void *stream);
 
-/* SmartNanogridEnv.step(actions) (smart_nanogrid_environment.py:149-197) for every env:
+/* Reseed: env i draws the streams of seed + global index i from the next reset on (reference RNG:
+ * np.random.seed / random.seed of that value; device RNG: the hash streams of that seed, from day 0).
+ * The loaded day stays loaded.  Synchronises `stream`. */
+int sng_set_seed(SngEnv *env, uint64_t seed, void *stream);
+
+/* SmartNanogridEnv.step(actions) (smart_nanogrid_environment.py:140-188) for every env:
  * one fused kernel.  reward = -total cost (f64), done = 1 at the end of the day.
  * `info` may be NULL.  Asynchronous on `stream`. */
 int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
              const SngInfo *info, void *stream);
 
-/* Sticky per-env error flags (SNG_FLAG_*), copied to host; synchronises. */
-int sng_read_errors(SngEnv *env, uint32_t *host_flags, int clear);
+/* The kernel name (as rocprofv3 reports it) of the step kernel sng_step would launch next with this
+ * `info` (NULL allowed): "void sng::step_kernel<NC, L, DIAG, FAST, PK>". */
+int sng_step_kernel_name(const SngEnv *env, const SngInfo *info, char *buf, int32_t len);
 
-/* State access for resume / parity injection (host arrays of num_envs doubles). */
-int sng_get_battery_soc(SngEnv *env, double *host_soc);
-int sng_set_battery_soc(SngEnv *env, const double *host_soc);
-int sng_get_pv_ratio(SngEnv *env, double *host_ratio);
-/* EV state of charge SOC[c, t] after the last step, host [num_envs][N]. */
-int sng_get_vehicle_soc(SngEnv *env, double *host_soc);
+/* Sticky per-env error flags (SNG_FLAG_*), copied to host after the work queued on `stream`;
+ * synchronises that stream only. */
+int sng_read_errors(SngEnv *env, uint32_t *host_flags, int clear, void *stream);
 
-/* The current day of env `env_index` in the reference's initial_values.json layout
- * (ChargingStation.generated_initial_values_json, charging_station.py:164-191), decoded from
- * the device timeline -- for host-generated, device-generated and injected days alike.
- * soc / occupancy / capacity / requested_soc: host [N][slots]; arrivals / departures: host
- * [N][max_vehicles], -1 padded (n_vehicles[N] holds the full counts); pv_ratio: one double.
+/* State access (host arrays of num_envs doubles; [num_envs][N] for the vehicle SoC), ordered after the
+ * work queued on `stream`; each synchronises that stream only.  Attribute reads of the reference's
+ * components: battery_energy_storage_system.py:108-109, random_pv_shift_ratio, charger.py:16. */
+int sng_get_battery_soc(SngEnv *env, double *host_soc, void *stream);
+int sng_set_battery_soc(SngEnv *env, const double *host_soc, void *stream);
+int sng_get_pv_ratio(SngEnv *env, double *host_ratio, void *stream);
+int sng_get_vehicle_soc(SngEnv *env, double *host_soc, void *stream);   /* SOC[c, t] of the last step */
+int sng_set_vehicle_soc(SngEnv *env, const double *host_soc, void *stream);
+
+/* Checkpoint / resume of the whole simulation: EV SoC [N][E], BESS SoC and the
+ * day's initial SoC (central_management_system.py:93-94), PV ratio, t = 0 penalty, sticky flags, the
+ * loaded day (timeline, requested-SoC stream, profile factors), the timestep, the device day counter,
+ * the replay bookkeeping, the reference RNG streams when they exist, and -- when episode_return is
+ * given (device [num_envs] f64, e.g. SngInfo.episode_return) -- the running day returns.  The blob is
+ * host memory of sng_state_size bytes; sng_set_state accepts only a blob of a handle with the same
+ * configuration, num_envs and ABI.  Both synchronise `stream`. */
+int sng_state_size(const SngEnv *env, int with_episode_return, size_t *bytes);
+int sng_get_state(SngEnv *env, void *host_buf, size_t bytes, const double *episode_return, void *stream);
+int sng_set_state(SngEnv *env, const void *host_buf, size_t bytes, double *episode_return, void *stream);
+
+/* The current day of envs [first, first + count) in the reference's initial_values.json layout
+ * (ChargingStation.generated_initial_values_json, charging_station.py:164-191), decoded from the device
+ * timeline -- for host-generated, device-generated and injected days alike.
+ * soc / occupancy / capacity / requested_soc: host [count][N][slots]; arrivals / departures: host
+ * [count][N][max_vehicles], -1 padded (n_vehicles[count][N] holds the full counts); pv_ratio: [count].
  * 'SOC' holds the arrival SoCs and the recorded SOC[c, t] of empty chargers (the slots a step
  * reads); Requested_SOC is exact when requested SoC is enabled or any penalised value differs
- * from 1.0, and 1.0 on occupied slots otherwise.  Valid after a reset until the next reset;
- * synchronises the device. */
-int sng_get_scenario(SngEnv *env, int64_t env_index, int32_t max_vehicles, double *soc, double *occupancy,
-                     double *capacity, double *requested_soc, int32_t *arrivals, int32_t *departures,
-                     int32_t *n_vehicles, double *pv_ratio);
+ * from 1.0, and 1.0 on occupied slots otherwise (0 everywhere on a replayed day).  Valid after a reset
+ * until the next reset; synchronises `stream`. */
+int sng_get_scenario(SngEnv *env, int64_t first, int64_t count, int32_t max_vehicles, double *soc,
+                     double *occupancy, double *capacity, double *requested_soc, int32_t *arrivals,
+                     int32_t *departures, int32_t *n_vehicles, double *pv_ratio, void *stream);
 
 /* Constant tables as built at create (host copies; n = 2*T). */
 int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_power, double *price,
@@ -236,9 +273,11 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
  * day_returns (device [days][num_envs] f64, may be NULL): day d's returns accumulate into row
  * d instead of info->episode_return, so a replay leaves every day's returns for one
  * collective per replay (bench.py gathers them over RCCL while the next replay runs).
- * Without SNG_GRAPH_RESET the graph steps whatever day is loaded at launch; device-RNG days and
- * host-RNG / injected days have different timeline encodings (sng_layout.h), so launching a
- * steps-only graph over a day of the other kind than at capture fails with SNG_ERR_STATE. */
+ * Without SNG_GRAPH_RESET the graph steps the day that is loaded at launch, from t = 0: device-RNG days,
+ * host-RNG / injected days and replayed days are stepped with different encodings (sng_layout.h:
+ * packed records, requested-SoC stream, cleared Requested_SOC, day-counter ownership), so launching a
+ * steps-only graph over a day of another encoding than at capture, or after t = 0, fails with
+ * SNG_ERR_STATE. */
 #define SNG_GRAPH_RESET 1   /* start every day with a device-RNG reset */
 int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
                      const SngInfo *info, int flags, int32_t days, double *day_returns, SngGraph **out);
@@ -257,6 +296,13 @@ int sng_host_generate_scenarios(const SngConfig *cfg, int64_t num_envs, uint64_t
                                 double *soc, double *occupancy, double *capacity, double *requested_soc,
                                 int32_t *arrivals, int32_t *departures, int32_t max_vehicles,
                                 double *pv_ratio);
+
+/* Host threads the reference-RNG generator and the scenario encoder use (see sng_reset). */
+int32_t sng_host_threads(void);
+
+/* The device day counter: the number of device-RNG days this handle has started (the next device
+ * reset draws day *out).  Synchronises `stream`. */
+int sng_get_day_counter(SngEnv *env, uint64_t *out, void *stream);
 
 #ifdef __cplusplus
 }

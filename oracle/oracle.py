@@ -49,6 +49,8 @@ def lib():
         L.orc_env_free.argtypes = [vp]
         L.orc_env_reset.restype = i
         L.orc_env_reset.argtypes = [vp, fp]
+        L.orc_env_replay.restype = i
+        L.orc_env_replay.argtypes = [vp, fp]
         L.orc_env_load.restype = i
         L.orc_env_load.argtypes = [vp, dp, dp, dp, dp, ip, ip, i, d, fp]
         L.orc_env_step_flat.restype = i
@@ -88,7 +90,7 @@ def _ptr(a, ct):
 
 
 def parse_time_interval(ti):
-    """smart_nanogrid_environment.py:134-147"""
+    """smart_nanogrid_environment.py:125-138"""
     if ti:
         if "h" in ti:
             return float(ti.replace("h", ""))
@@ -103,7 +105,7 @@ def irradiance():
 
 
 class OracleConfig:
-    """Same keyword names as the reference SmartNanogridEnv.__init__ (smart_nanogrid_environment.py:41-43)."""
+    """Same keyword names as the reference SmartNanogridEnv.__init__ (smart_nanogrid_environment.py:32-34)."""
 
     def __init__(self, price_model=0, number_of_chargers=8, pv_system_available_in_model=True,
                  battery_system_available_in_model=True, vehicle_to_everything=False,
@@ -181,6 +183,13 @@ class OracleEnv:
     def reset(self):
         obs = np.zeros(self.cfg.obs_dim, np.float32)
         lib().orc_env_reset(self.ptr, _ptr(obs, ctypes.c_float))
+        return obs
+
+    def replay(self):
+        """reset(generate_new_initial_values=False): the last generated day again (load_initial_values)."""
+        obs = np.zeros(self.cfg.obs_dim, np.float32)
+        if lib().orc_env_replay(self.ptr, _ptr(obs, ctypes.c_float)) < 0:
+            raise RuntimeError("oracle: no generated day to replay")
         return obs
 
     def load(self, soc, occ, cap, req, arrivals, departures, ratio):

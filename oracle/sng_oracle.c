@@ -188,24 +188,24 @@ enum { PEN_NONE = 0, PEN_ON_DEPARTURE = 1, PEN_SPARSE = 2, PEN_DENSE = 3, PEN_IN
 typedef struct {
     int n_chargers;          /* number_of_chargers */
     int T;                   /* int(24 / dt) */
-    double dt;               /* set_time_interval, smart_nanogrid_environment.py:134-147 */
+    double dt;               /* set_time_interval, smart_nanogrid_environment.py:125-138 */
     int pv, bess, v2x;
     int diff_caps;           /* enable_different_vehicle_battery_capacities */
     int req_enabled;         /* enable_requested_state_of_charge */
     int penalty_mode;        /* charging_station.py:50-60 */
     int bounded;             /* charging_mode == 'bounded' */
     int numpy_legacy;        /* 1: NumPy<2 promotion (action*22*0.95 in f64) */
-    double grid_cost_weight; /* accountant.py:222 (0.75 in v1; 0.8 in the recorded KATs) */
+    double grid_cost_weight; /* accountant.py:35 (0.75 in v1; 0.8 in the recorded KATs) */
     int extended;            /* build-defined extended day (see above) */
     int slots;               /* per-charger array length: 25 (charger.py:16-19), T+1 when extended */
     double pv_noise, price_noise;
     /* tables, built by orc_build_tables */
     int n_irr;
-    double irr[4 * ORC_MAXT];       /* solar_irradiance_2[0, :], pv_system_manager.py:322-353 */
+    double irr[4 * ORC_MAXT];       /* solar_irradiance_2[0, :], pv_system_manager.py:34-65 */
     double irr_max;
-    double pv_power[4 * ORC_MAXT];  /* available_solar_power[0, :], :355-376 */
+    double pv_power[4 * ORC_MAXT];  /* available_solar_power[0, :], :67-91 */
     int n_price;
-    double price[4 * ORC_MAXT];     /* energy_price[0, :], accountant.py:235-288 (48 entries) */
+    double price[4 * ORC_MAXT];     /* energy_price[0, :], accountant.py:48-101 (48 entries) */
     double price_max;
 } orc_cfg;
 
@@ -234,27 +234,27 @@ static double pairwise_sum(const double *a, long n) {
 
 double orc_pairwise_sum(const double *a, long n) { return pairwise_sum(a, n); }
 
-/* PVSystemManager (pv_system_manager.py:10-91) + Accountant (accountant.py:204-288).
+/* PVSystemManager (pv_system_manager.py:10-91) + Accountant (accountant.py:17-101).
  * Returns 0, or -1 for a price model the reference cannot build. */
 int orc_build_tables(orc_cfg *c, int price_model, const double *irr_min, long n_min) {
     int T = c->T;
-    int steps_min = (int)(60 * c->dt);                 /* :323 */
-    int padded = T * 2;                                /* 1 prediction day + 1 padding day, :300-303 */
+    int steps_min = (int)(60 * c->dt);                 /* pv_system_manager.py:35 */
+    int padded = T * 2;                                /* 1 prediction day + 1 padding day, :11-15 */
     c->n_irr = padded;
     for (int k = 0; k < padded; k++) {
         long lo = (long)k * steps_min, hi = lo + steps_min;
         if (hi > n_min) hi = n_min;
         long cnt = hi - lo;
-        c->irr[k] = cnt > 0 ? pairwise_sum(irr_min + lo, cnt) / (double)cnt : NAN;  /* mean(), :330 */
+        c->irr[k] = cnt > 0 ? pairwise_sum(irr_min + lo, cnt) / (double)cnt : NAN;  /* mean(), :42 */
     }
-    double mx = 0.0;                                   /* max(where >= 0, initial=0), :308 */
+    double mx = 0.0;                                   /* max(where >= 0, initial=0), :20 */
     for (int k = 0; k < padded; k++) if (c->irr[k] >= 0 && c->irr[k] > mx) mx = c->irr[k];
     c->irr_max = mx;
-    double scaling_pv = ((2.279 * 1.134) * 20) * 0.21 / 1000;   /* :305, :360-361 */
+    double scaling_pv = ((2.279 * 1.134) * 20) * 0.21 / 1000;   /* :17, :72-73 */
     for (int k = 0; k < padded; k++)
-        c->pv_power[k] = ((c->irr[k] * scaling_pv) * 1.5) / c->dt;  /* :355-358, :375-376 */
+        c->pv_power[k] = ((c->irr[k] * scaling_pv) * 1.5) / c->dt;  /* :67-70, :87-88 */
 
-    double high = (0.028 + 0.148933333) + 0.014;       /* set_grid_tariffs, :204-211 */
+    double high = (0.028 + 0.148933333) + 0.014;       /* set_grid_tariffs, accountant.py:17-24 */
     double low = (0.013333333 + 0.087613333) + 0.014;
     static const double m1[24] = {0.05, 0.05, 0.05, 0.05, 0.05, 0.05, 0.05, 0.1, 0.1, 0.1, 0.1, 0.1,
                                   0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 0.1, 0.05, 0.05, 0.05, 0.05};
@@ -266,16 +266,16 @@ int orc_build_tables(orc_cfg *c, int price_model, const double *irr_min, long n_
                                   0.1, 0.1, 0.1, 0.1, 0.1, 0.06, 0.06, 0.06, 0.1, 0.1, 0.1, 0.1};
     double day[24];
     switch (price_model) {
-        case 0: for (int h = 0; h < 24; h++) day[h] = (h < 7 || h >= 20) ? low : high; break; /* :256-260 */
+        case 0: for (int h = 0; h < 24; h++) day[h] = (h < 7 || h >= 20) ? low : high; break; /* :69-73 */
         case 1: memcpy(day, m1, sizeof day); break;
         case 2: memcpy(day, m2, sizeof day); break;
         case 3: memcpy(day, m3, sizeof day); break;
         case 4: memcpy(day, m4, sizeof day); break;
-        default: return -1;   /* model 5 raises TypeError (:277-278), others a shape error */
+        default: return -1;   /* model 5 raises TypeError (:90-98), others a shape error */
     }
     if (!c->extended) {
         c->n_price = 48;
-        for (int k = 0; k < 48; k++) c->price[k] = day[k % 24];   /* concatenate twice, :287 */
+        for (int k = 0; k < 48; k++) c->price[k] = day[k % 24];   /* concatenate twice, :100 */
     } else {
         /* per-step tariffs: the loop of accountant.py:61-68 for model 0, the hourly value otherwise */
         c->n_price = 2 * T;
@@ -289,7 +289,7 @@ int orc_build_tables(orc_cfg *c, int price_model, const double *irr_min, long n_
     }
     mx = 0.0;
     for (int k = 0; k < c->n_price; k++) if (c->price[k] >= 0 && c->price[k] > mx) mx = c->price[k];
-    c->price_max = mx;                                   /* :238 */
+    c->price_max = mx;                                   /* accountant.py:51 */
     return 0;
 }
 
@@ -310,12 +310,16 @@ typedef struct {
     uint64_t day;                   /* resets so far (profile noise key) */
     int t;
     double ratio;                   /* random_pv_shift_ratio */
-    double bess_soc, bess_init;     /* battery_energy_storage_system.py:166-178, initial 0.5 */
+    double bess_soc, bess_init;     /* battery_energy_storage_system.py:6-22, initial 0.5 */
     double bess_power, bess_calc_power;
     int penalty_list[ORC_MAXN], n_penalty;  /* ChargingStation._penalty_check_vehicles */
     double f_pv[ORC_MAXT + 4], f_price[ORC_MAXT + 4];   /* this day's profile factors */
     orc_charger *ch;
     double *slotbuf;
+    /* the last generated day, as initial_values.json holds it (charging_station.py:185-186) */
+    orc_charger *gen;
+    double *gen_slotbuf;
+    int has_gen;
 } orc_env;
 
 /* Step record (the 28-key results dict subset the parity tests compare). */
@@ -348,10 +352,17 @@ orc_env *orc_env_new(const orc_cfg *c, uint64_t seed) {
     e->cfg = c;
     e->ch = (orc_charger *)calloc((size_t)c->n_chargers, sizeof(orc_charger));
     e->slotbuf = (double *)calloc((size_t)c->n_chargers * 4 * c->slots, sizeof(double));
-    if (!e->ch || !e->slotbuf) { free(e->ch); free(e->slotbuf); free(e); return NULL; }
+    e->gen = (orc_charger *)calloc((size_t)c->n_chargers, sizeof(orc_charger));
+    e->gen_slotbuf = (double *)calloc((size_t)c->n_chargers * 4 * c->slots, sizeof(double));
+    if (!e->ch || !e->slotbuf || !e->gen || !e->gen_slotbuf) {
+        free(e->ch); free(e->slotbuf); free(e->gen); free(e->gen_slotbuf); free(e);
+        return NULL;
+    }
     for (int i = 0; i < c->n_chargers; i++) {
         double *b = e->slotbuf + (size_t)i * 4 * c->slots;
         e->ch[i].soc = b; e->ch[i].cap = b + c->slots; e->ch[i].occ = b + 2 * c->slots; e->ch[i].req = b + 3 * c->slots;
+        double *g = e->gen_slotbuf + (size_t)i * 4 * c->slots;
+        e->gen[i].soc = g; e->gen[i].cap = g + c->slots; e->gen[i].occ = g + 2 * c->slots; e->gen[i].req = g + 3 * c->slots;
     }
     orc_np_seed(&e->np_rng, (uint32_t)seed);
     orc_py_seed(&e->py_rng, seed);
@@ -359,7 +370,7 @@ orc_env *orc_env_new(const orc_cfg *c, uint64_t seed) {
     e->day = 0;
     e->bess_soc = 0.5;     /* central_management_system.py:35 */
     e->bess_init = 0.5;
-    e->ratio = 1.0;        /* smart_nanogrid_environment.py:74 */
+    e->ratio = 1.0;        /* smart_nanogrid_environment.py:65 */
     return e;
 }
 
@@ -367,7 +378,18 @@ void orc_env_free(orc_env *e) {
     if (!e) return;
     free(e->ch);
     free(e->slotbuf);
+    free(e->gen);
+    free(e->gen_slotbuf);
     free(e);
+}
+
+/* copy one charger's day (slot arrays and arrival/departure lists) */
+static void charger_copy(int S, orc_charger *dst, const orc_charger *src) {
+    memcpy(dst->soc, src->soc, sizeof(double) * S); memcpy(dst->cap, src->cap, sizeof(double) * S);
+    memcpy(dst->occ, src->occ, sizeof(double) * S); memcpy(dst->req, src->req, sizeof(double) * S);
+    memcpy(dst->arrivals, src->arrivals, sizeof dst->arrivals); dst->n_arr = src->n_arr;
+    memcpy(dst->departures, src->departures, sizeof dst->departures); dst->n_dep = src->n_dep;
+    dst->nonexistent = src->nonexistent;
 }
 
 /* The day's profile factors (build-defined; all 1.0 when both sigmas are 0). */
@@ -459,7 +481,7 @@ static void penalty_check(orc_env *e, int t) {
 }
 
 /* CentralManagementSystem.observe + SmartNanogridEnv.__get_observations
- * (central_management_system.py:45-78, smart_nanogrid_environment.py:199-240) */
+ * (central_management_system.py:45-78, smart_nanogrid_environment.py:190-231) */
 static int observe(orc_env *e, float *obs) {
     const orc_cfg *c = e->cfg;
     int t = e->t, N = c->n_chargers, k = 0;
@@ -486,16 +508,39 @@ static int observe(orc_env *e, float *obs) {
 }
 
 /* ChargingStation.clear_initialisation_variables + generate_new_initial_values
- * (charging_station.py:138-186), then SmartNanogridEnv.reset (smart_nanogrid_environment.py:320-360). */
+ * (charging_station.py:138-186), then SmartNanogridEnv.reset (smart_nanogrid_environment.py:311-351). */
 int orc_env_reset(orc_env *e, float *obs) {
     const orc_cfg *c = e->cfg;
     e->t = 0;
     for (int i = 0; i < c->n_chargers; i++) {
         charger_clear(e, &e->ch[i]);
         gen_charger(e, &e->ch[i]);
+        charger_copy(c->slots, &e->gen[i], &e->ch[i]);   /* json.dump(initial_values.json), :185-186 */
     }
-    e->ratio = (double)orc_py_randint(&e->py_rng, 0, 180) / 100;   /* :358 */
+    e->has_gen = 1;
+    e->ratio = (double)orc_py_randint(&e->py_rng, 0, 180) / 100;   /* :349 */
     draw_profiles(e);
+    return observe(e, obs);
+}
+
+/* SmartNanogridEnv.reset(generate_new_initial_values=False) (smart_nanogrid_environment.py:311-357):
+ * ChargingStation.load_initial_values (charging_station.py:119-136) clears the chargers
+ * (clear_initialisation_variables, :138-150) and reads back what the last generation wrote to
+ * initial_values.json (:185-186): arrivals, departures, SOC, occupancy and capacities -- but not
+ * Requested_SOC, which stays 0.  Then a new PV ratio from the Python stream (:349); the numpy stream
+ * and the BESS are untouched, the day's profile factors are kept.  Returns -1 when no day was
+ * generated (the reference would read whatever file is on disk). */
+int orc_env_replay(orc_env *e, float *obs) {
+    const orc_cfg *c = e->cfg;
+    if (!e->has_gen) return -1;
+    e->t = 0;
+    for (int i = 0; i < c->n_chargers; i++) {
+        orc_charger *ch = &e->ch[i];
+        charger_copy(c->slots, ch, &e->gen[i]);
+        memset(ch->req, 0, sizeof(double) * c->slots);
+        ch->nonexistent = 0.0;
+    }
+    e->ratio = (double)orc_py_randint(&e->py_rng, 0, 180) / 100;
     return observe(e, obs);
 }
 
@@ -586,7 +631,7 @@ static double vehicle_penalty(double req, double cur) {
 }
 
 /* SmartNanogridEnv.step -> CentralManagementSystem.manage_nanogrid
- * (smart_nanogrid_environment.py:149-197, central_management_system.py:84-185) */
+ * (smart_nanogrid_environment.py:140-188, central_management_system.py:84-185) */
 int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out) {
     const orc_cfg *c = e->cfg;
     int N = c->n_chargers, t = e->t;
@@ -631,7 +676,7 @@ int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out
     else if (demand < 0 && c->v2x) out->breakpoint = 1;                 /* :160-165 */
     double rem = demand - solar;                                        /* :167 */
     double pen_b = 0.0;
-    if (c->bess) {                                                      /* battery_energy_storage_system.py:186-262 */
+    if (c->bess) {                                                      /* battery_energy_storage_system.py:30-106 */
         if (ba == 0) {
             e->bess_power = 0.0; e->bess_calc_power = 0.0;
         } else if (!c->bounded) {
@@ -648,7 +693,7 @@ int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out
             double dp = (ba * 44) * 0.95;
             double calc = e->bess_soc + (dp * c->dt) / 80;
             e->bess_calc_power = dp;
-            if (calc < 0) dp = -((e->bess_soc * 80) / c->dt);          /* :238-250 */
+            if (calc < 0) dp = -((e->bess_soc * 80) / c->dt);          /* :82-94 */
             e->bess_soc = (calc > 0.0) ? calc : 0.0;
             e->bess_power = dp;
             rem = rem + dp;
@@ -661,9 +706,9 @@ int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out
     double grid = rem;
     double energy = grid * c->dt;                                       /* :107 */
     double price = c->price[t] * e->f_price[t];
-    double cost = energy < 0 ? (energy * 0.8) * price : energy * price; /* accountant.py:213-219 */
+    double cost = energy < 0 ? (energy * 0.8) * price : energy * price; /* accountant.py:26-32 */
     double total_pen = 0.8 * pen_b + pen_v;                             /* penaliser.py:177-181 */
-    double total = c->grid_cost_weight * fabs(cost) + total_pen;        /* accountant.py:221-223 */
+    double total = c->grid_cost_weight * fabs(cost) + total_pen;        /* accountant.py:34-36 */
 
     out->reward = -total;
     out->grid_power = grid; out->p_charge = p_ch; out->p_discharge = p_dis;
@@ -676,9 +721,9 @@ int orc_env_step(orc_env *e, const float *actions, float *obs, orc_step_out *out
     out->bess_initial_soc = c->bess ? e->bess_init : 0.0;
     out->error = err;
 
-    observe(e, obs);                                                    /* :182 */
+    observe(e, obs);                                                    /* smart_nanogrid_environment.py:173 */
     e->t = t + 1;
-    if ((double)e->t == 24.0 / c->dt) {                                 /* :185-190, :242-246 */
+    if ((double)e->t == 24.0 / c->dt) {                                 /* :174-181, :233-237 */
         out->done = 1;
         e->t = 0;
         e->ratio = (double)orc_py_randint(&e->py_rng, 0, 180) / 100;

@@ -3,13 +3,19 @@
 // Owns the per-handle device state, builds the constant tables, turns days in the
 // reference's own layout (25-slot arrays + arrival/departure lists) into the packed
 // per-charger-step words the step kernel reads, generates reference-exact days on host
-// threads (MT19937 streams), and captures whole days into hipGraphs.
+// threads (MT19937 streams) while uploading them, replays the last generated day, saves and
+// restores the whole simulation state, and captures whole days into hipGraphs.
 #include <hip/hip_runtime.h>
+#include <sched.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -23,13 +29,14 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
                        double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
                        hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
-                           int vec_io, hipStream_t stream);
+                           int vec_io, hipStream_t stream, int mode, int64_t replay);
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            float *obs, double *ep_return, int vec_io,
                            hipStream_t stream);
 hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream);
 hipError_t launch_bump_day(const DeviceState &s, hipStream_t stream);
 int step_lanes_supported(int n, int lanes);
+int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len);
 }  // namespace sng
 
 using namespace sng;
@@ -41,7 +48,7 @@ thread_local std::string g_create_error;
 constexpr int kMaxVehicles = 32;
 
 // numpy pairwise_sum (contiguous float64), used by ndarray.mean() in
-// PVSystemManager.calculate_solar_irradiance_mean (pv_system_manager.py:322-332)
+// PVSystemManager.calculate_solar_irradiance_mean (pv_system_manager.py:34-44)
 double pairwise_sum(const double *a, long n) {
     if (n < 8) {
         double res = 0.0;
@@ -68,7 +75,7 @@ struct HostTables {
     double irr_max = 0, price_max = 0;
 };
 
-// PVSystemManager (pv_system_manager.py:10-91) and Accountant price tables (accountant.py:204-288)
+// PVSystemManager (pv_system_manager.py:10-91) and Accountant price tables (accountant.py:17-101)
 bool build_tables(const SngConfig &c, int T, HostTables &tb, std::string &err) {
     const double dt = c.time_interval_hours;
     const int steps_min = (int)(60 * dt);
@@ -85,10 +92,10 @@ bool build_tables(const SngConfig &c, int T, HostTables &tb, std::string &err) {
     for (double v : tb.irr)
         if (v >= 0 && v > mx) mx = v;
     tb.irr_max = mx;
-    const double scaling_pv = ((2.279 * 1.134) * 20) * 0.21 / 1000;   // PVSystem(...), :305, :360-361
+    const double scaling_pv = ((2.279 * 1.134) * 20) * 0.21 / 1000;   // PVSystem(...), pv_system_manager.py:17, :72-73
     for (int k = 0; k < padded; ++k) tb.pv_power[k] = ((tb.irr[k] * scaling_pv) * 1.5) / dt;
 
-    const double high = (0.028 + 0.148933333) + 0.014;   // set_grid_tariffs, accountant.py:204-211
+    const double high = (0.028 + 0.148933333) + 0.014;   // set_grid_tariffs, accountant.py:17-24
     const double low = (0.013333333 + 0.087613333) + 0.014;
     static const double m1[24] = {0.05, 0.05, 0.05, 0.05, 0.05, 0.05, 0.05, 0.1, 0.1, 0.1, 0.1, 0.1,
                                   0.1,  0.1,  0.1,  0.1,  0.1,  0.1,  0.1,  0.1, 0.05, 0.05, 0.05, 0.05};
@@ -101,19 +108,19 @@ bool build_tables(const SngConfig &c, int T, HostTables &tb, std::string &err) {
     double day[24];
     switch (c.price_model) {
         case 0:
-            for (int h = 0; h < 24; ++h) day[h] = (h < 7 || h >= 20) ? low : high;   // :256-260
+            for (int h = 0; h < 24; ++h) day[h] = (h < 7 || h >= 20) ? low : high;   // accountant.py:69-73
             break;
         case 1: std::memcpy(day, m1, sizeof day); break;
         case 2: std::memcpy(day, m2, sizeof day); break;
         case 3: std::memcpy(day, m3, sizeof day); break;
         case 4: std::memcpy(day, m4, sizeof day); break;
         default:
-            err = "price_model must be 0..4 (model 5 raises TypeError in accountant.py:277-278)";
+            err = "price_model must be 0..4 (model 5 raises TypeError in accountant.py:90-98)";
             return false;
     }
     if (!c.extended_day) {
         tb.price.assign(kPriceLen, 0.0);
-        for (int k = 0; k < kPriceLen; ++k) tb.price[k] = day[k % 24];   // concatenate([day, day]), :287
+        for (int k = 0; k < kPriceLen; ++k) tb.price[k] = day[k % 24];   // concatenate([day, day]), accountant.py:100
     } else {
         // build-defined extended day: the per-step tariff loop of accountant.py:61-68 for model 0,
         // the hourly value of hour floor(i*dt) for models 1-4; concatenated twice
@@ -311,22 +318,32 @@ bool encode_day(const Params &p, int64_t E, int64_t e, const DayView &d, uint32_
     return true;
 }
 
-template <class F>
-void parallel_for(int64_t n, F &&f) {
-    unsigned hw = std::thread::hardware_concurrency();
-    int64_t nt = std::max<int64_t>(1, std::min<int64_t>({(int64_t)(hw ? hw : 4), (int64_t)16, (n + 255) / 256}));
-    if (nt == 1) {
-        f(0, n, 0);
-        return;
+// Host threads for the reference-RNG day generator and the scenario encoder: the CPUs this process
+// may run on (sched_getaffinity), capped by SNG_HOST_THREADS or OMP_NUM_THREADS when set (a GPU box
+// shows the whole machine's CPUs but gives one process a share of them).
+int host_threads() {
+    int n = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) n = CPU_COUNT(&set);
+    if (n <= 0) n = (int)std::thread::hardware_concurrency();
+    for (const char *var : {"SNG_HOST_THREADS", "OMP_NUM_THREADS"}) {
+        const char *v = std::getenv(var);
+        if (v && std::atoi(v) > 0) {
+            n = std::min(n, std::atoi(v));
+            break;
+        }
     }
-    std::vector<std::thread> th;
-    const int64_t chunk = (n + nt - 1) / nt;
-    for (int64_t k = 0; k < nt; ++k) {
-        const int64_t b = k * chunk, en = std::min(n, b + chunk);
-        if (b >= en) break;
-        th.emplace_back([&, b, en, k] { f(b, en, (int)k); });
+    return std::max(1, std::min(n, 64));
+}
+
+// FNV-1a over a byte range (the checkpoint's configuration fingerprint)
+uint64_t fnv1a(const void *data, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char *b = static_cast<const unsigned char *>(data);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
     }
-    for (auto &x : th) x.join();
+    return h;
 }
 
 }  // namespace
@@ -335,14 +352,21 @@ struct SngEnv {
     SngConfig cfg{};
     Params p{};
     HostTables tables;
+    Tables host_tab{};                // what d_tables holds
+    uint64_t cfg_hash = 0;            // configuration fingerprint (scalars + tables), checked by sng_set_state
     std::vector<double> irradiance;   // owned copy
     int device = 0;
     int64_t E = 0;
     uint64_t seed = 0;
     int t = -1;                       // -1: never reset; T: day finished
-    bool day_finished = false;
+    bool day_finished = false;        // the reference's end-of-day Python draw (:181) is still owed
     int i4 = 0, i10 = 0, i1 = 0;
     int slots = kSlots;               // per-charger array length of scenarios (T+1 with extended_day)
+    // the day reset(generate_new_initial_values=False) replays: the last day sng_reset generated
+    // (the reference's initial_values.json, charging_station.py:185-186 / :119-136)
+    int gen_mode = -1;                // -1: none yet; else the SngRngMode that generated it
+    bool gen_loaded = false;          // its timeline is still the loaded one (no injected day since)
+    uint64_t replays = 0;             // device-RNG replays so far: the replay ratio stream's counter
     DeviceState ds{};
     Tables *d_tables = nullptr;
     // host staging (pinned) for days built on the CPU
@@ -356,10 +380,20 @@ struct SngEnv {
     size_t timeline() const { return (size_t)p.T * p.n * (size_t)E; }
 };
 
+// The Params fields that say how the loaded day is encoded and stepped; a steps-only graph
+// captures them and may replay only over a day with the same key.
+struct DayKey {
+    int32_t packed, req_stream, req_zero, bump_day;
+    bool operator==(const DayKey &o) const {
+        return packed == o.packed && req_stream == o.req_stream && req_zero == o.req_zero && bump_day == o.bump_day;
+    }
+};
+static DayKey day_key(const Params &p) { return DayKey{p.packed, p.req_stream, p.req_zero, p.bump_day}; }
+
 struct SngGraph {
     SngEnv *env = nullptr;
     bool with_reset = false;
-    int packed = 0;   // the timeline encoding the graph's steps read
+    DayKey key{};   // the loaded-day encoding the graph's steps were captured for
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
 };
@@ -431,27 +465,143 @@ int ensure_staging(SngEnv *env, bool with_req) {
     return SNG_OK;
 }
 
-// Upload the staged day, then the t = 0 observation.
-int upload_and_observe(SngEnv *env, bool need_req, float *obs, hipStream_t st) {
-    const size_t n = env->timeline();
-    HIP_TRY(env, hipMemcpyAsync(env->ds.word, env->h_word, n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-    HIP_TRY(env, hipMemcpyAsync(env->ds.aux, env->h_aux, n * sizeof(double), hipMemcpyHostToDevice, st));
-    if (need_req) {
-        int rc = ensure_req(env);
-        if (rc) return rc;
-        HIP_TRY(env, hipMemcpyAsync(env->ds.req, env->h_req, n * sizeof(double), hipMemcpyHostToDevice, st));
+// The reference's global RNG streams of every env: np.random.seed(s) and random.seed(s) with
+// s = seed + global env index (SngRngMode SNG_RNG_REFERENCE).
+void ensure_streams(SngEnv *env) {
+    if (!env->np_rng.empty()) return;
+    env->np_rng.resize(env->E);
+    env->py_rng.resize(env->E);
+    for (int64_t i = 0; i < env->E; ++i) {
+        const uint64_t s = env->seed + (uint64_t)env->p.env_offset + (uint64_t)i;
+        env->np_rng[i].seed_numpy((uint32_t)s);
+        env->py_rng[i].seed_python(s);
     }
+}
+
+// Per-thread scratch for one env's day in the reference layout.
+struct DayScratch {
+    std::vector<double> soc, occ, cap, req;
+    std::vector<int32_t> arr, dep;
+    DayView view(int N, int S, int V) {
+        soc.assign((size_t)N * S, 0.0);
+        occ.assign((size_t)N * S, 0.0);
+        cap.assign((size_t)N * S, 0.0);
+        req.assign((size_t)N * S, 0.0);
+        arr.assign((size_t)N * V, -1);
+        dep.assign((size_t)N * V, -1);
+        return DayView{soc.data(), occ.data(), cap.data(), req.data(), arr.data(), dep.data(), V, S};
+    }
+};
+
+// Build every env's day on host threads and upload it while the rest is still being built:
+// workers take chunks of envs and encode them into the pinned [T][N][E] staging planes; as soon as
+// chunk k (in order) is encoded, this thread enqueues its columns of the planes as one 2D copy per
+// plane.  build(i, scratch, need_req, err) builds env i.  req_upload: the requested-SoC plane goes
+// up with the chunks (1), after the last chunk if any env needs it (-1: decided by need_req), or
+// not at all (0).  Returns SNG_OK or an error; *need_req_out reports whether any env needed it.
+template <class Build>
+int build_and_upload(SngEnv *env, int req_upload, hipStream_t st, bool *need_req_out, Build &&build) {
+    const int64_t E = env->E;
+    const int N = env->p.n, T = env->p.T;
+    const size_t rows = (size_t)T * N;
+    const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, E / 256));
+    const int64_t chunk = std::max<int64_t>(256, (E + 4 * nt - 1) / (4 * nt));   // ~4 chunks per thread
+    const int64_t nchunks = (E + chunk - 1) / chunk;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<int> state((size_t)nchunks, 0);   // 0 pending, 1 encoded, 2 failed
+    std::vector<std::string> errs((size_t)nchunks);
+    std::atomic<int64_t> next{0};
+    std::atomic<bool> stop{false}, need_req{false};
+    auto worker = [&]() {
+        DayScratch scratch;
+        for (;;) {
+            const int64_t k = next.fetch_add(1);
+            if (k >= nchunks) return;
+            int st_k = 1;
+            std::string e;
+            bool nr = false;
+            if (stop.load()) {
+                st_k = 2;
+                e = "cancelled";
+            } else {
+                const int64_t b = k * chunk, en = std::min(E, b + chunk);
+                for (int64_t i = b; i < en; ++i)
+                    if (!build(i, scratch, &nr, e)) {
+                        st_k = 2;
+                        stop.store(true);
+                        break;
+                    }
+            }
+            if (nr) need_req.store(true);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                state[(size_t)k] = st_k;
+                errs[(size_t)k] = e;
+            }
+            cv.notify_one();
+        }
+    };
+    std::vector<std::thread> th;
+    for (int w = 0; w < nt; ++w) th.emplace_back(worker);
+    int rc = SNG_OK;
+    std::string msg;
+    for (int64_t k = 0; k < nchunks && rc == SNG_OK; ++k) {
+        int st_k;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return state[(size_t)k] != 0; });
+            st_k = state[(size_t)k];
+            msg = errs[(size_t)k];
+        }
+        if (st_k != 1) {
+            rc = SNG_ERR_INVALID_ARGUMENT;
+            break;
+        }
+        const int64_t b = k * chunk, w = std::min(E, b + chunk) - b;
+        hipError_t e = hipMemcpy2DAsync(env->ds.word + b, E * sizeof(uint32_t), env->h_word + b, E * sizeof(uint32_t),
+                                        w * sizeof(uint32_t), rows, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = hipMemcpy2DAsync(env->ds.aux + b, E * sizeof(double), env->h_aux + b, E * sizeof(double),
+                                 w * sizeof(double), rows, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess && req_upload == 1)
+            e = hipMemcpy2DAsync(env->ds.req + b, E * sizeof(double), env->h_req + b, E * sizeof(double),
+                                 w * sizeof(double), rows, hipMemcpyHostToDevice, st);
+        if (e != hipSuccess) {
+            rc = SNG_ERR_HIP;
+            msg = std::string("staged upload: ") + hipGetErrorString(e);
+        }
+    }
+    stop.store(rc != SNG_OK);
+    for (auto &x : th) x.join();
+    if (rc != SNG_OK) return fail(env, rc, msg);
+    *need_req_out = need_req.load();
+    if (req_upload == -1 && *need_req_out) {
+        int r = ensure_req(env);
+        if (r) return r;
+        HIP_TRY(env, hipMemcpyAsync(env->ds.req, env->h_req, env->timeline() * sizeof(double),
+                                    hipMemcpyHostToDevice, st));
+    }
+    return SNG_OK;
+}
+
+// After the day's planes: the PV ratios and t = 0 penalties, then the t = 0 observation.
+int finish_host_day(SngEnv *env, bool req_stream, float *obs, hipStream_t st) {
     HIP_TRY(env, hipMemcpyAsync(env->ds.ratio, env->h_ratio, env->E * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipMemcpyAsync(env->ds.pen0, env->h_pen0, env->E * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipEventRecord(env->staging_done, st));
-    env->p.req_stream = need_req ? 1 : 0;
+    env->p.req_stream = req_stream ? 1 : 0;
     env->p.packed = 0;   // word + f64 aux planes
+    env->p.req_zero = 0;
+    env->p.bump_day = 0;
     HIP_TRY(env, sng::launch_profiles(env->p, env->ds, env->E, st));
-    HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st));
+    HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st, OBS0_HOST, -1));
     env->t = 0;
     env->day_finished = false;
     return SNG_OK;
 }
+
+hipStream_t as_stream(void *s) { return (hipStream_t)s; }
 
 }  // namespace
 
@@ -462,8 +612,8 @@ int32_t sng_abi_version(void) { return SNG_ABI_VERSION; }
 void sng_config_defaults(SngConfig *c) {
     std::memset(c, 0, sizeof *c);
     c->abi_version = SNG_ABI_VERSION;
-    c->number_of_chargers = 8;                 // smart_nanogrid_environment.py:41
-    c->time_interval_hours = 1.0;              // :147
+    c->number_of_chargers = 8;                 // smart_nanogrid_environment.py:32
+    c->time_interval_hours = 1.0;              // :138
     c->price_model = 0;
     c->pv_system_available = 1;
     c->battery_system_available = 1;
@@ -473,9 +623,9 @@ void sng_config_defaults(SngConfig *c) {
     c->charging_mode_bounded = 1;
     c->penalty_mode = SNG_PENALTY_SPARSE;
     c->numpy_legacy_promotion = 0;
-    c->grid_cost_weight = 0.75;                // accountant.py:222
+    c->grid_cost_weight = 0.75;                // accountant.py:35
     c->battery_penalty_weight = 0.8;           // penaliser.py:181
-    c->selling_price_coefficient = 0.8;        // accountant.py:193
+    c->selling_price_coefficient = 0.8;        // accountant.py:6
     c->bess_capacity_kwh = 80;                 // central_management_system.py:35
     c->bess_initial_soc = 0.5;
     c->bess_max_charging_kw = 44;
@@ -566,8 +716,8 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
     p.diff_caps = c.different_vehicle_capacities ? 1 : 0;
     p.req_enabled = c.requested_state_of_charge ? 1 : 0;
     p.req_stream = p.req_enabled;
-    p.obs_dim = (1 + p.pv) * 4 + 2 * p.n + p.bess;   // smart_nanogrid_environment.py:99-105
-    p.act_dim = p.n + p.bess;                          // :110-127
+    p.obs_dim = (1 + p.pv) * 4 + 2 * p.n + p.bess;   // smart_nanogrid_environment.py:90-96
+    p.act_dim = p.n + p.bess;                          // :101-118
     p.dt = c.time_interval_hours;
     p.dt_f = (float)c.time_interval_hours;
     {
@@ -609,20 +759,29 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
     p.seed = seed;
 
     // host copy of the device tables
-    Tables ht;
+    Tables &ht = env->host_tab;
     std::memset(&ht, 0, sizeof ht);
     const int n_irr = (int)env->tables.irr.size();
     ht.n_irr = n_irr;
     for (int k = 0; k < n_irr; ++k) {
-        ht.irr_norm[k] = env->tables.irr[k] / env->tables.irr_max;   // pv_system_manager.py:369-373
+        ht.irr_norm[k] = env->tables.irr[k] / env->tables.irr_max;   // pv_system_manager.py:81-85
         ht.pv_power[k] = env->tables.pv_power[k];
     }
     for (int k = 0; k < (int)env->tables.price.size(); ++k) {
         ht.price[k] = env->tables.price[k];
-        ht.price_norm[k] = env->tables.price[k] / env->tables.price_max;   // accountant.py:229-233
+        ht.price_norm[k] = env->tables.price[k] / env->tables.price_max;   // accountant.py:42-46
     }
     ht.recip[0] = 0.0;
     for (int c = 1; c < 256; ++c) ht.recip[c] = 1.0 / (double)c;
+    {
+        // checkpoint fingerprint: every configuration scalar that changes the simulation, and the tables
+        SngConfig k = c;
+        k.irradiance_per_minute = nullptr;
+        k.irradiance_minutes = 0;
+        k.step_lanes_per_env = 0;
+        k.reserved0 = 0;
+        env->cfg_hash = fnv1a(&ht, sizeof ht, fnv1a(&k, sizeof k));
+    }
 
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) {
@@ -710,15 +869,33 @@ int sng_set_env_offset(SngEnv *env, int64_t offset) {
     return SNG_OK;
 }
 
+int sng_set_seed(SngEnv *env, uint64_t seed, void *stream) {
+    if (!env) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null handle");
+    HIP_TRY(env, hipSetDevice(env->device));
+    env->seed = seed;
+    env->p.seed = seed;
+    env->np_rng.clear();   // re-seeded (seed + offset + i) at the next reset
+    env->py_rng.clear();
+    env->day_finished = false;
+    env->replays = 0;
+    // device days restart at day 0 of the new streams; the loaded day stays loaded
+    HIP_TRY(env, hipMemsetAsync(env->ds.episode, 0, sizeof(uint64_t), as_stream(stream)));
+    if (env->p.packed && env->t == 0) env->p.bump_day = 0;   // an unstepped device day no longer owns day 0
+    HIP_TRY(env, hipStreamSynchronize(as_stream(stream)));
+    return SNG_OK;
+}
+
 int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     if (!env || !obs) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     HIP_TRY(env, hipSetDevice(env->device));
-    hipStream_t st = (hipStream_t)stream;
+    hipStream_t st = as_stream(stream);
     if (rng_mode == SNG_RNG_DEVICE) {
         if (!device_rng_ok(env)) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
-        const bool unstepped_device_day = env->p.packed && env->t == 0;
+        const bool unstepped_device_day = env->p.packed && env->p.bump_day && env->t == 0;
         env->p.req_stream = env->p.req_enabled;
         env->p.packed = 1;   // the generator writes packed records (sng_layout.h)
+        env->p.req_zero = 0;
+        env->p.bump_day = 1;
         if (env->p.req_stream) {
             int rc = ensure_req(env);
             if (rc) return rc;
@@ -730,54 +907,81 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
                                      aligned16(obs) ? 1 : 0, st));
         env->t = 0;
         env->day_finished = false;
+        env->gen_mode = SNG_RNG_DEVICE;
+        env->gen_loaded = true;
         return SNG_OK;
     }
     if (rng_mode != SNG_RNG_REFERENCE) return fail(env, SNG_ERR_INVALID_ARGUMENT, "unknown rng_mode");
 
-    const int N = env->p.n, T = env->p.T;
-    const bool first = env->np_rng.empty();
-    if (first) {
-        env->np_rng.resize(env->E);
-        env->py_rng.resize(env->E);
-        for (int64_t i = 0; i < env->E; ++i) {
-            const uint64_t s = env->seed + (uint64_t)env->p.env_offset + (uint64_t)i;
-            env->np_rng[i].seed_numpy((uint32_t)s);
-            env->py_rng[i].seed_python(s);
-        }
-    }
+    const int N = env->p.n, T = env->p.T, S = env->slots;
+    ensure_streams(env);
     const bool with_req = env->p.req_enabled != 0;
+    if (with_req) {
+        int rc = ensure_req(env);
+        if (rc) return rc;
+    }
     int rc = ensure_staging(env, with_req);
     if (rc) return rc;
     const bool end_draw = env->day_finished;
-    std::vector<std::string> errs(16);
-    std::vector<char> bad(16, 0);
-    parallel_for(env->E, [&](int64_t b, int64_t en, int k) {
-        const int V = kMaxVehicles, S = env->slots;
-        std::vector<double> soc(N * S), occ(N * S), cap(N * S), req(N * S);
-        std::vector<int32_t> arr(N * V), dep(N * V);
-        DayView d{soc.data(), occ.data(), cap.data(), req.data(), arr.data(), dep.data(), V, S};
-        bool need = false;
-        for (int64_t i = b; i < en; ++i) {
-            // the day-end draw of the previous step (smart_nanogrid_environment.py:190)
+    bool need = false;
+    rc = build_and_upload(env, with_req ? 1 : 0, st, &need,
+                          [&](int64_t i, DayScratch &sc, bool *nr, std::string &e) -> bool {
+                              DayView d = sc.view(N, S, kMaxVehicles);
+                              // the day-end draw of the previous step (smart_nanogrid_environment.py:181)
+                              if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
+                              if (!generate_day(env->cfg, T, env->np_rng[i], d)) {
+                                  e = "more vehicles per charger than supported";
+                                  return false;
+                              }
+                              env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;   // :349
+                              return encode_day(env->p, env->E, i, d, env->h_word, env->h_aux,
+                                                with_req ? env->h_req : nullptr, &env->h_pen0[i], nr, e);
+                          });
+    if (rc) return rc;
+    rc = finish_host_day(env, with_req, obs, st);
+    if (rc) return rc;
+    env->gen_mode = SNG_RNG_REFERENCE;
+    env->gen_loaded = true;
+    return SNG_OK;
+}
+
+int sng_reset_replay(SngEnv *env, float *obs, void *stream) {
+    if (!env || !obs) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    if (env->gen_mode < 0 || !env->gen_loaded)
+        return fail(env, SNG_ERR_STATE,
+                    env->gen_mode < 0 ? "reset(generate_new_initial_values=False) replays the last generated day "
+                                        "(initial_values.json, charging_station.py:185-186): none was generated yet"
+                                      : "reset(generate_new_initial_values=False) replays the last generated day; an "
+                                        "injected day (sng_reset_from_scenario) has replaced it since");
+    HIP_TRY(env, hipSetDevice(env->device));
+    hipStream_t st = as_stream(stream);
+    const int vec = aligned16(obs) ? 1 : 0;
+    if (env->gen_mode == SNG_RNG_REFERENCE) {
+        // a new random_pv_shift_ratio from each env's Python stream (smart_nanogrid_environment.py:349),
+        // after the day-end draw the last step still owes (:181); the numpy stream is not touched
+        ensure_streams(env);
+        int rc = ensure_staging(env, false);
+        if (rc) return rc;
+        const bool end_draw = env->day_finished;
+        for (int64_t i = 0; i < env->E; ++i) {
             if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
-            if (!generate_day(env->cfg, T, env->np_rng[i], d)) {
-                bad[k] = 1;
-                errs[k] = "more vehicles per charger than supported";
-                return;
-            }
-            env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;   // :358
-            std::string e;
-            if (!encode_day(env->p, env->E, i, d, env->h_word, env->h_aux, with_req ? env->h_req : nullptr,
-                            &env->h_pen0[i], &need, e)) {
-                bad[k] = 1;
-                errs[k] = e;
-                return;
-            }
+            env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;
         }
-    });
-    for (int k = 0; k < 16; ++k)
-        if (bad[k]) return fail(env, SNG_ERR_INVALID_ARGUMENT, errs[k]);
-    return upload_and_observe(env, with_req, obs, st);
+        HIP_TRY(env, hipMemcpyAsync(env->ds.ratio, env->h_ratio, env->E * sizeof(double), hipMemcpyHostToDevice, st));
+        HIP_TRY(env, hipEventRecord(env->staging_done, st));
+        env->p.req_zero = 1;
+        env->p.bump_day = 0;
+        HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, vec, st, OBS0_REPLAY, -1));
+    } else {
+        env->p.req_zero = 1;
+        env->p.bump_day = 0;
+        HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, vec, st, OBS0_REPLAY,
+                                          (int64_t)env->replays));
+        env->replays += 1;
+    }
+    env->t = 0;
+    env->day_finished = false;
+    return SNG_OK;
 }
 
 int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void *stream) {
@@ -786,38 +990,50 @@ int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void
         return fail(env, SNG_ERR_INVALID_ARGUMENT,
                     "scenario slots must be " + std::to_string(env->slots) + " (25; T+1 with extended_day)");
     if (!sc->soc || !sc->occupancy || !sc->capacity || !sc->requested_soc || !sc->arrivals || !sc->departures ||
-        !sc->pv_ratio || sc->max_vehicles < 1)
+        sc->max_vehicles < 1)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "incomplete scenario");
     HIP_TRY(env, hipSetDevice(env->device));
     int rc = ensure_staging(env, true);
     if (rc) return rc;
-    const int N = env->p.n, V = sc->max_vehicles;
-    std::vector<std::string> errs(16);
-    std::vector<char> bad(16, 0), need(16, 0);
-    parallel_for(env->E, [&](int64_t b, int64_t en, int k) {
-        bool nr = false;
-        for (int64_t i = b; i < en; ++i) {
-            const int S = env->slots;
-            const size_t o = (size_t)i * N * S, ol = (size_t)i * N * V;
-            DayView d{const_cast<double *>(sc->soc + o), const_cast<double *>(sc->occupancy + o),
-                      const_cast<double *>(sc->capacity + o), const_cast<double *>(sc->requested_soc + o),
-                      const_cast<int32_t *>(sc->arrivals + ol), const_cast<int32_t *>(sc->departures + ol), V, S};
-            std::string e;
-            if (!encode_day(env->p, env->E, i, d, env->h_word, env->h_aux, env->h_req, &env->h_pen0[i], &nr, e)) {
-                bad[k] = 1;
-                errs[k] = "env " + std::to_string(i) + ": " + e;
-                return;
-            }
-            env->h_ratio[i] = sc->pv_ratio[i];
-        }
-        need[k] = nr;
-    });
-    bool need_req = env->p.req_enabled != 0;
-    for (int k = 0; k < 16; ++k) {
-        if (bad[k]) return fail(env, SNG_ERR_INVALID_ARGUMENT, errs[k]);
-        need_req = need_req || need[k];
+    // Python-stream accounting (env i == the reference seeded seed + i): the day-end draw the last
+    // step still owes (smart_nanogrid_environment.py:181), and, when no ratio is given, the reset's own
+    // draw (:349) -- what reset(generate_new_initial_values=False) consumes
+    const bool draw_ratio = sc->pv_ratio == nullptr;
+    if (draw_ratio) ensure_streams(env);
+    const bool streams = !env->py_rng.empty();
+    const bool end_draw = env->day_finished && streams;
+    const int N = env->p.n, V = sc->max_vehicles, S = env->slots;
+    // the requested-SoC plane goes up with the chunks when the config enables it (the step reads it
+    // then), else only if some penalised slot of the given days is not 1.0
+    const bool req_enabled = env->p.req_enabled != 0;
+    if (req_enabled) {
+        rc = ensure_req(env);
+        if (rc) return rc;
     }
-    return upload_and_observe(env, need_req, obs, (hipStream_t)stream);
+    bool need = false;
+    rc = build_and_upload(env, req_enabled ? 1 : -1, as_stream(stream), &need,
+                          [&](int64_t i, DayScratch &, bool *nr, std::string &e) -> bool {
+                              const size_t o = (size_t)i * N * S, ol = (size_t)i * N * V;
+                              DayView d{const_cast<double *>(sc->soc + o), const_cast<double *>(sc->occupancy + o),
+                                        const_cast<double *>(sc->capacity + o),
+                                        const_cast<double *>(sc->requested_soc + o),
+                                        const_cast<int32_t *>(sc->arrivals + ol),
+                                        const_cast<int32_t *>(sc->departures + ol), V, S};
+                              if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
+                              env->h_ratio[i] = draw_ratio ? (double)env->py_rng[i].py_randint(0, 180) / 100
+                                                           : sc->pv_ratio[i];
+                              if (!encode_day(env->p, env->E, i, d, env->h_word, env->h_aux, env->h_req,
+                                              &env->h_pen0[i], nr, e)) {
+                                  e = "env " + std::to_string(i) + ": " + e;
+                                  return false;
+                              }
+                              return true;
+                          });
+    if (rc) return rc;
+    rc = finish_host_day(env, req_enabled || need, obs, as_stream(stream));
+    if (rc) return rc;
+    env->gen_loaded = false;   // the generated day a replay restores is no longer loaded
+    return SNG_OK;
 }
 
 int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done, const SngInfo *info,
@@ -828,132 +1044,172 @@ int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint
     HIP_TRY(env, hipSetDevice(env->device));
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
     HIP_TRY(env, launch_step(env->p, env->ds, info_ptrs(info), actions, obs, reward, done, env->E, env->t, vec,
-                             (hipStream_t)stream));
+                             as_stream(stream)));
     env->t += 1;
     if (env->t == env->p.T) env->day_finished = true;
     return SNG_OK;
 }
 
-int sng_read_errors(SngEnv *env, uint32_t *host_flags, int clear) {
+int sng_step_kernel_name(const SngEnv *env, const SngInfo *info, char *buf, int32_t len) {
+    if (!env || !buf || len < 1) return SNG_ERR_INVALID_ARGUMENT;
+    const int n = step_kernel_name(env->p, info_ptrs(info), buf, len);
+    return (n > 0 && n < len) ? SNG_OK : SNG_ERR_INVALID_ARGUMENT;
+}
+
+int sng_read_errors(SngEnv *env, uint32_t *host_flags, int clear, void *stream) {
     if (!env || !host_flags) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     HIP_TRY(env, hipSetDevice(env->device));
-    HIP_TRY(env, hipDeviceSynchronize());
-    HIP_TRY(env, hipMemcpy(host_flags, env->ds.flags, env->E * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    if (clear) HIP_TRY(env, hipMemset(env->ds.flags, 0, env->E * sizeof(uint32_t)));
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(env, hipMemcpyAsync(host_flags, env->ds.flags, env->E * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (clear) HIP_TRY(env, hipMemsetAsync(env->ds.flags, 0, env->E * sizeof(uint32_t), st));
+    HIP_TRY(env, hipStreamSynchronize(st));
     return SNG_OK;
 }
 
-int sng_get_battery_soc(SngEnv *env, double *h) {
-    if (!env || !h) return SNG_ERR_INVALID_ARGUMENT;
+// One per-env f64 array between the device and the host, ordered on `stream` (the caller's work on it
+// completes first); synchronises that stream only.
+static int copy_env_array(SngEnv *env, double *dev, double *host, bool to_host, void *stream, const char *what) {
+    if (!env) return SNG_ERR_INVALID_ARGUMENT;
+    if (!host) return fail(env, SNG_ERR_INVALID_ARGUMENT, std::string(what) + ": null host array");
     HIP_TRY(env, hipSetDevice(env->device));
-    HIP_TRY(env, hipDeviceSynchronize());
-    HIP_TRY(env, hipMemcpy(h, env->ds.bess, env->E * sizeof(double), hipMemcpyDeviceToHost));
+    hipStream_t st = as_stream(stream);
+    if (to_host)
+        HIP_TRY(env, hipMemcpyAsync(host, dev, env->E * sizeof(double), hipMemcpyDeviceToHost, st));
+    else
+        HIP_TRY(env, hipMemcpyAsync(dev, host, env->E * sizeof(double), hipMemcpyHostToDevice, st));
+    HIP_TRY(env, hipStreamSynchronize(st));
     return SNG_OK;
 }
 
-int sng_set_battery_soc(SngEnv *env, const double *h) {
-    if (!env || !h) return SNG_ERR_INVALID_ARGUMENT;
-    HIP_TRY(env, hipSetDevice(env->device));
-    HIP_TRY(env, hipDeviceSynchronize());
-    HIP_TRY(env, hipMemcpy(env->ds.bess, h, env->E * sizeof(double), hipMemcpyHostToDevice));
-    return SNG_OK;
+int sng_get_battery_soc(SngEnv *env, double *h, void *stream) {
+    return env ? copy_env_array(env, env->ds.bess, h, true, stream, "sng_get_battery_soc") : SNG_ERR_INVALID_ARGUMENT;
 }
 
-int sng_get_pv_ratio(SngEnv *env, double *h) {
-    if (!env || !h) return SNG_ERR_INVALID_ARGUMENT;
-    HIP_TRY(env, hipSetDevice(env->device));
-    HIP_TRY(env, hipDeviceSynchronize());
-    HIP_TRY(env, hipMemcpy(h, env->ds.ratio, env->E * sizeof(double), hipMemcpyDeviceToHost));
-    return SNG_OK;
+int sng_set_battery_soc(SngEnv *env, const double *h, void *stream) {
+    return env ? copy_env_array(env, env->ds.bess, const_cast<double *>(h), false, stream, "sng_set_battery_soc")
+               : SNG_ERR_INVALID_ARGUMENT;
 }
 
-int sng_get_vehicle_soc(SngEnv *env, double *h) {
-    if (!env || !h) return SNG_ERR_INVALID_ARGUMENT;
+int sng_get_pv_ratio(SngEnv *env, double *h, void *stream) {
+    return env ? copy_env_array(env, env->ds.ratio, h, true, stream, "sng_get_pv_ratio") : SNG_ERR_INVALID_ARGUMENT;
+}
+
+int sng_get_vehicle_soc(SngEnv *env, double *h, void *stream) {
+    if (!env) return SNG_ERR_INVALID_ARGUMENT;
+    if (!h) return fail(env, SNG_ERR_INVALID_ARGUMENT, "sng_get_vehicle_soc: null host array");
     HIP_TRY(env, hipSetDevice(env->device));
-    HIP_TRY(env, hipDeviceSynchronize());
     const int N = env->p.n;
+    hipStream_t st = as_stream(stream);
+    // [N][E] on the device -> [E][N] on the host
     std::vector<double> tmp((size_t)N * env->E);
-    HIP_TRY(env, hipMemcpy(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost));
+    HIP_TRY(env, hipMemcpyAsync(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_TRY(env, hipStreamSynchronize(st));
     for (int64_t e = 0; e < env->E; ++e)
         for (int c = 0; c < N; ++c) h[e * N + c] = tmp[(size_t)c * env->E + e];
     return SNG_OK;
 }
 
-// Inverse of encode_day / generate_kernel for one env: the word stream gives occupancy,
-// capacity and (at each arrival, W_STATIC on an occupied step) the departure; aux gives the
-// arrival SoC and the SOC[c, t] of empty chargers; the req stream holds Requested_SOC[c, t-1]
-// at t >= 1 and Requested_SOC[c, T-1] at t = 0.
-int sng_get_scenario(SngEnv *env, int64_t e, int32_t V, double *soc, double *occupancy, double *capacity,
-                     double *requested_soc, int32_t *arrivals, int32_t *departures, int32_t *n_vehicles,
-                     double *pv_ratio) {
+int sng_set_vehicle_soc(SngEnv *env, const double *h, void *stream) {
+    if (!env) return SNG_ERR_INVALID_ARGUMENT;
+    if (!h) return fail(env, SNG_ERR_INVALID_ARGUMENT, "sng_set_vehicle_soc: null host array");
+    HIP_TRY(env, hipSetDevice(env->device));
+    const int N = env->p.n;
+    std::vector<double> tmp((size_t)N * env->E);
+    for (int64_t e = 0; e < env->E; ++e)
+        for (int c = 0; c < N; ++c) tmp[(size_t)c * env->E + e] = h[e * N + c];
+    hipStream_t st = as_stream(stream);
+    HIP_TRY(env, hipMemcpyAsync(env->ds.soc, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice, st));
+    HIP_TRY(env, hipStreamSynchronize(st));
+    return SNG_OK;
+}
+
+// Inverse of encode_day / generate_kernel for envs [first, first + count): the word stream gives
+// occupancy, capacity and (at each arrival, W_STATIC on an occupied step) the departure; aux gives the
+// arrival SoC and the SOC[c, t] of empty chargers; the req stream holds Requested_SOC[c, t-1] at
+// t >= 1 and Requested_SOC[c, T-1] at t = 0.  The env range's columns of each plane come over in one
+// 2D copy.
+int sng_get_scenario(SngEnv *env, int64_t first, int64_t count, int32_t V, double *soc, double *occupancy,
+                     double *capacity, double *requested_soc, int32_t *arrivals, int32_t *departures,
+                     int32_t *n_vehicles, double *pv_ratio, void *stream) {
     if (!env || !soc || !occupancy || !capacity || !requested_soc || !arrivals || !departures || !n_vehicles ||
         !pv_ratio)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
-    if (e < 0 || e >= env->E || V < 1) return fail(env, SNG_ERR_INVALID_ARGUMENT, "env_index or max_vehicles out of range");
+    if (first < 0 || count < 1 || first + count > env->E || V < 1)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "env range or max_vehicles out of range");
     if (env->t < 0) return fail(env, SNG_ERR_STATE, "no day yet: call reset()");
     HIP_TRY(env, hipSetDevice(env->device));
-    HIP_TRY(env, hipDeviceSynchronize());
+    hipStream_t st = as_stream(stream);
     const int N = env->p.n, T = env->p.T, S = env->slots;
-    const size_t rows = (size_t)T * N, pitch = (size_t)env->E;
-    std::vector<uint32_t> w(rows);
-    std::vector<double> aux(rows), rq;
+    const size_t rows = (size_t)T * N, pitch = (size_t)env->E, cnt = (size_t)count;
+    std::vector<uint32_t> w(rows * cnt);
+    std::vector<double> aux(rows * cnt), rq;
+    std::vector<uint64_t> rec;
     if (env->p.packed) {   // device-RNG day: packed records in the aux buffer (sng_layout.h)
-        std::vector<uint64_t> rec(rows);
-        HIP_TRY(env, hipMemcpy2D(rec.data(), sizeof(uint64_t), reinterpret_cast<const uint64_t *>(env->ds.aux) + e,
-                                 pitch * sizeof(uint64_t), sizeof(uint64_t), rows, hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < rows; ++i) {
+        rec.resize(rows * cnt);
+        HIP_TRY(env, hipMemcpy2DAsync(rec.data(), cnt * sizeof(uint64_t),
+                                      reinterpret_cast<const uint64_t *>(env->ds.aux) + first, pitch * sizeof(uint64_t),
+                                      cnt * sizeof(uint64_t), rows, hipMemcpyDeviceToHost, st));
+    } else {
+        HIP_TRY(env, hipMemcpy2DAsync(w.data(), cnt * sizeof(uint32_t), env->ds.word + first, pitch * sizeof(uint32_t),
+                                      cnt * sizeof(uint32_t), rows, hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipMemcpy2DAsync(aux.data(), cnt * sizeof(double), env->ds.aux + first, pitch * sizeof(double),
+                                      cnt * sizeof(double), rows, hipMemcpyDeviceToHost, st));
+    }
+    const bool have_req = env->p.req_stream && !env->p.req_zero && env->ds.req;
+    if (have_req) {
+        rq.resize(rows * cnt);
+        HIP_TRY(env, hipMemcpy2DAsync(rq.data(), cnt * sizeof(double), env->ds.req + first, pitch * sizeof(double),
+                                      cnt * sizeof(double), rows, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(env, hipMemcpyAsync(pv_ratio, env->ds.ratio + first, cnt * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_TRY(env, hipStreamSynchronize(st));
+    if (env->p.packed) {
+        for (size_t i = 0; i < rec.size(); ++i) {
             w[i] = (uint32_t)rec[i];
             const uint32_t hi = (uint32_t)(rec[i] >> 32);
             float f;
             std::memcpy(&f, &hi, sizeof f);
             aux[i] = (double)f;
         }
-    } else {
-        HIP_TRY(env, hipMemcpy2D(w.data(), sizeof(uint32_t), env->ds.word + e, pitch * sizeof(uint32_t),
-                                 sizeof(uint32_t), rows, hipMemcpyDeviceToHost));
-        HIP_TRY(env, hipMemcpy2D(aux.data(), sizeof(double), env->ds.aux + e, pitch * sizeof(double), sizeof(double),
-                                 rows, hipMemcpyDeviceToHost));
     }
-    const bool have_req = env->p.req_stream && env->ds.req;
-    if (have_req) {
-        rq.resize(rows);
-        HIP_TRY(env, hipMemcpy2D(rq.data(), sizeof(double), env->ds.req + e, pitch * sizeof(double), sizeof(double),
-                                 rows, hipMemcpyDeviceToHost));
-    }
-    HIP_TRY(env, hipMemcpy(pv_ratio, env->ds.ratio + e, sizeof(double), hipMemcpyDeviceToHost));
-    std::fill(soc, soc + (size_t)N * S, 0.0);
-    std::fill(occupancy, occupancy + (size_t)N * S, 0.0);
-    std::fill(capacity, capacity + (size_t)N * S, 0.0);
-    std::fill(requested_soc, requested_soc + (size_t)N * S, 0.0);
-    std::fill(arrivals, arrivals + (size_t)N * V, -1);
-    std::fill(departures, departures + (size_t)N * V, -1);
-    for (int c = 0; c < N; ++c) {
-        int nv = 0;
-        for (int t = 0; t < T; ++t) {
-            const size_t i = (size_t)t * N + c;
-            const uint32_t word = w[i];
-            const bool occ = (word & W_OCC) != 0;
-            const size_t o = (size_t)c * S + t;
-            if (occ) {
-                occupancy[o] = 1.0;
-                capacity[o] = (double)((word >> W_CAP_SHIFT) & 0xffu);
-                if (word & W_STATIC) {   // arrival: SOC[c, t] as generated, departure t + remaining
-                    soc[o] = aux[i];
-                    if (nv < V) {
-                        arrivals[(size_t)c * V + nv] = t;
-                        departures[(size_t)c * V + nv] = t + (int)((word >> W_DEP_SHIFT) & 0xffu);
+    for (size_t k = 0; k < cnt; ++k) {
+        double *soc_k = soc + k * N * S, *occ_k = occupancy + k * N * S, *cap_k = capacity + k * N * S;
+        double *req_k = requested_soc + k * N * S;
+        int32_t *arr_k = arrivals + k * N * V, *dep_k = departures + k * N * V, *nv_k = n_vehicles + k * N;
+        std::fill(soc_k, soc_k + (size_t)N * S, 0.0);
+        std::fill(occ_k, occ_k + (size_t)N * S, 0.0);
+        std::fill(cap_k, cap_k + (size_t)N * S, 0.0);
+        std::fill(req_k, req_k + (size_t)N * S, 0.0);
+        std::fill(arr_k, arr_k + (size_t)N * V, -1);
+        std::fill(dep_k, dep_k + (size_t)N * V, -1);
+        for (int c = 0; c < N; ++c) {
+            int nv = 0;
+            for (int t = 0; t < T; ++t) {
+                const size_t i = ((size_t)t * N + c) * cnt + k;
+                const uint32_t word = w[i];
+                const bool occ = (word & W_OCC) != 0;
+                const size_t o = (size_t)c * S + t;
+                if (occ) {
+                    occ_k[o] = 1.0;
+                    cap_k[o] = (double)((word >> W_CAP_SHIFT) & 0xffu);
+                    if (word & W_STATIC) {   // arrival: SOC[c, t] as generated, departure t + remaining
+                        soc_k[o] = aux[i];
+                        if (nv < V) {
+                            arr_k[(size_t)c * V + nv] = t;
+                            dep_k[(size_t)c * V + nv] = t + (int)((word >> W_DEP_SHIFT) & 0xffu);
+                        }
+                        ++nv;
                     }
-                    ++nv;
+                } else {
+                    soc_k[o] = aux[i];
                 }
-            } else {
-                soc[o] = aux[i];
+                if (have_req)
+                    req_k[o] = rq[((t + 1 < T ? (size_t)(t + 1) * N : 0) + c) * cnt + k];
+                else   // a replayed day keeps the cleared zeros (charging_station.py:138-150)
+                    req_k[o] = (occ && !env->p.req_zero) ? 1.0 : 0.0;
             }
-            if (have_req)
-                requested_soc[o] = rq[(t + 1 < T ? (size_t)(t + 1) * N : 0) + c];
-            else
-                requested_soc[o] = occ ? 1.0 : 0.0;
+            nv_k[c] = nv;
         }
-        n_vehicles[c] = nv;
     }
     return SNG_OK;
 }
@@ -968,6 +1224,180 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
     if (irr_max) *irr_max = tb.irr_max;
     if (price_max) *price_max = tb.price_max;
     if (n) *n = (int32_t)tb.irr.size();
+    return SNG_OK;
+}
+
+// ---------------------------------------------------------------------------------
+// Checkpoint / resume: header, then the sections in this order (host byte order):
+//   soc f64[N][E] | bess, bess0, ratio, pen0 f64[E] | flags u32[E] | [word u32[T][N][E], host days]
+//   | aux 8B[T][N][E] | [req f64[T][N][E]] | [prof f64[2][T+3][E]] | [episode return f64[E]]
+//   | [reference streams u32[E][2][625]]
+// ---------------------------------------------------------------------------------
+struct StateHeader {
+    char magic[8];
+    int32_t abi, header_bytes;
+    int64_t num_envs;
+    int32_t n, T, slots, obs_dim;
+    uint64_t config_hash, seed;
+    int64_t env_offset;
+    int32_t t, day_finished;
+    int32_t packed, req_stream, req_zero, bump_day;
+    int32_t gen_mode, gen_loaded;
+    uint64_t replays, day_counter;
+    int32_t has_word, has_req, has_prof, has_return, has_streams, reserved;
+    uint64_t total_bytes;
+};
+static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '2'};
+
+static StateHeader state_layout(const SngEnv *env, bool with_return) {
+    StateHeader h{};
+    std::memcpy(h.magic, kStateMagic, sizeof h.magic);
+    h.abi = SNG_ABI_VERSION;
+    h.header_bytes = (int32_t)sizeof(StateHeader);
+    h.num_envs = env->E;
+    h.n = env->p.n;
+    h.T = env->p.T;
+    h.slots = env->slots;
+    h.obs_dim = env->p.obs_dim;
+    h.config_hash = env->cfg_hash;
+    h.seed = env->seed;
+    h.env_offset = env->p.env_offset;
+    h.t = env->t;
+    h.day_finished = env->day_finished ? 1 : 0;
+    h.packed = env->p.packed;
+    h.req_stream = env->p.req_stream;
+    h.req_zero = env->p.req_zero;
+    h.bump_day = env->p.bump_day;
+    h.gen_mode = env->gen_mode;
+    h.gen_loaded = env->gen_loaded ? 1 : 0;
+    h.replays = env->replays;
+    h.has_word = env->p.packed ? 0 : 1;
+    h.has_req = (env->ds.req && env->p.req_stream) ? 1 : 0;
+    h.has_prof = env->ds.prof ? 1 : 0;
+    h.has_return = with_return ? 1 : 0;
+    h.has_streams = env->np_rng.empty() ? 0 : 1;
+    const size_t E = (size_t)env->E, tl = env->timeline();
+    size_t b = sizeof(StateHeader) + (size_t)env->p.n * E * 8 + 4 * E * 8 + E * 4 + tl * 8;
+    if (h.has_word) b += tl * 4;
+    if (h.has_req) b += tl * 8;
+    if (h.has_prof) b += 2 * (size_t)(env->p.T + 3) * E * 8;
+    if (h.has_return) b += E * 8;
+    if (h.has_streams) b += E * 2 * MT19937::kStateWords * 4;
+    h.total_bytes = b;
+    return h;
+}
+
+int sng_state_size(const SngEnv *env, int with_return, size_t *bytes) {
+    if (!env || !bytes) return SNG_ERR_INVALID_ARGUMENT;
+    *bytes = (size_t)state_layout(env, with_return != 0).total_bytes;
+    return SNG_OK;
+}
+
+int sng_get_state(SngEnv *env, void *buf, size_t bytes, const double *episode_return, void *stream) {
+    if (!env || !buf) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    HIP_TRY(env, hipSetDevice(env->device));
+    hipStream_t st = as_stream(stream);
+    StateHeader h = state_layout(env, episode_return != nullptr);
+    if (bytes < h.total_bytes) return fail(env, SNG_ERR_INVALID_ARGUMENT, "state buffer too small (sng_state_size)");
+    const size_t E = (size_t)env->E, tl = env->timeline();
+    char *out = static_cast<char *>(buf) + sizeof(StateHeader);
+    auto pull = [&](const void *dev, size_t n) -> hipError_t {
+        hipError_t e = hipMemcpyAsync(out, dev, n, hipMemcpyDeviceToHost, st);
+        out += n;
+        return e;
+    };
+    HIP_TRY(env, hipMemcpyAsync(&h.day_counter, env->ds.episode, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(env, pull(env->ds.soc, (size_t)env->p.n * E * 8));
+    HIP_TRY(env, pull(env->ds.bess, E * 8));
+    HIP_TRY(env, pull(env->ds.bess0, E * 8));
+    HIP_TRY(env, pull(env->ds.ratio, E * 8));
+    HIP_TRY(env, pull(env->ds.pen0, E * 8));
+    HIP_TRY(env, pull(env->ds.flags, E * 4));
+    if (h.has_word) HIP_TRY(env, pull(env->ds.word, tl * 4));
+    HIP_TRY(env, pull(env->ds.aux, tl * 8));
+    if (h.has_req) HIP_TRY(env, pull(env->ds.req, tl * 8));
+    if (h.has_prof) HIP_TRY(env, pull(env->ds.prof, 2 * (size_t)(env->p.T + 3) * E * 8));
+    if (h.has_return) HIP_TRY(env, pull(episode_return, E * 8));
+    HIP_TRY(env, hipStreamSynchronize(st));
+    if (h.has_streams) {
+        uint32_t *w = reinterpret_cast<uint32_t *>(out);
+        for (size_t i = 0; i < E; ++i) {
+            env->np_rng[i].save(w + (2 * i) * MT19937::kStateWords);
+            env->py_rng[i].save(w + (2 * i + 1) * MT19937::kStateWords);
+        }
+    }
+    std::memcpy(buf, &h, sizeof h);
+    return SNG_OK;
+}
+
+int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_return, void *stream) {
+    if (!env || !buf) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
+    if (bytes < sizeof(StateHeader)) return fail(env, SNG_ERR_INVALID_ARGUMENT, "not an sng state");
+    StateHeader h;
+    std::memcpy(&h, buf, sizeof h);
+    if (std::memcmp(h.magic, kStateMagic, sizeof h.magic) != 0 || h.abi != SNG_ABI_VERSION ||
+        h.header_bytes != (int32_t)sizeof(StateHeader))
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "not an sng state of this ABI version");
+    if (h.num_envs != env->E || h.n != env->p.n || h.T != env->p.T || h.slots != env->slots ||
+        h.obs_dim != env->p.obs_dim || h.config_hash != env->cfg_hash)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "state of a handle with another configuration or size");
+    if (h.total_bytes > bytes) return fail(env, SNG_ERR_INVALID_ARGUMENT, "truncated state");
+    if (h.has_return && !episode_return)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "the state holds day returns: pass an episode_return array");
+    if ((h.has_prof != 0) != (env->ds.prof != nullptr)) return fail(env, SNG_ERR_INVALID_ARGUMENT, "profile mismatch");
+    if (h.t < -1 || h.t > env->p.T) return fail(env, SNG_ERR_INVALID_ARGUMENT, "bad timestep in state");
+    HIP_TRY(env, hipSetDevice(env->device));
+    hipStream_t st = as_stream(stream);
+    if (h.has_req) {
+        int rc = ensure_req(env);
+        if (rc) return rc;
+    }
+    const size_t E = (size_t)env->E, tl = env->timeline();
+    const char *in = static_cast<const char *>(buf) + sizeof(StateHeader);
+    auto push = [&](void *dev, size_t n) -> hipError_t {
+        hipError_t e = hipMemcpyAsync(dev, in, n, hipMemcpyHostToDevice, st);
+        in += n;
+        return e;
+    };
+    // the restored streams, checked before anything is changed
+    std::vector<MT19937> np_rng, py_rng;
+    if (h.has_streams) {
+        const size_t off = h.total_bytes - E * 2 * MT19937::kStateWords * 4;
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(static_cast<const char *>(buf) + off);
+        np_rng.resize(E);
+        py_rng.resize(E);
+        for (size_t i = 0; i < E; ++i)
+            if (!np_rng[i].load(w + (2 * i) * MT19937::kStateWords) ||
+                !py_rng[i].load(w + (2 * i + 1) * MT19937::kStateWords))
+                return fail(env, SNG_ERR_INVALID_ARGUMENT, "corrupt RNG stream state");
+    }
+    HIP_TRY(env, hipMemcpyAsync(env->ds.episode, &h.day_counter, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+    HIP_TRY(env, push(env->ds.soc, (size_t)env->p.n * E * 8));
+    HIP_TRY(env, push(env->ds.bess, E * 8));
+    HIP_TRY(env, push(env->ds.bess0, E * 8));
+    HIP_TRY(env, push(env->ds.ratio, E * 8));
+    HIP_TRY(env, push(env->ds.pen0, E * 8));
+    HIP_TRY(env, push(env->ds.flags, E * 4));
+    if (h.has_word) HIP_TRY(env, push(env->ds.word, tl * 4));
+    HIP_TRY(env, push(env->ds.aux, tl * 8));
+    if (h.has_req) HIP_TRY(env, push(env->ds.req, tl * 8));
+    if (h.has_prof) HIP_TRY(env, push(env->ds.prof, 2 * (size_t)(env->p.T + 3) * E * 8));
+    if (h.has_return) HIP_TRY(env, push(episode_return, E * 8));
+    HIP_TRY(env, hipStreamSynchronize(st));
+    env->seed = h.seed;
+    env->p.seed = h.seed;
+    env->p.env_offset = h.env_offset;
+    env->t = h.t;
+    env->day_finished = h.day_finished != 0;
+    env->p.packed = h.packed;
+    env->p.req_stream = h.req_stream;
+    env->p.req_zero = h.req_zero;
+    env->p.bump_day = h.bump_day;
+    env->gen_mode = h.gen_mode;
+    env->gen_loaded = h.gen_loaded != 0;
+    env->replays = h.replays;
+    env->np_rng = std::move(np_rng);
+    env->py_rng = std::move(py_rng);
     return SNG_OK;
 }
 
@@ -989,12 +1419,14 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
     SngGraph *g = new SngGraph();
     g->env = env;
     Params p = env->p;
-    if (with_reset) {
+    if (with_reset) {   // every day a freshly generated device day (sng_reset(SNG_RNG_DEVICE))
         p.req_stream = p.req_enabled;
         p.packed = 1;
+        p.req_zero = 0;
+        p.bump_day = 1;
     }
     g->with_reset = with_reset;
-    g->packed = p.packed;
+    g->key = day_key(p);
     const InfoPtrs ip = info_ptrs(info);
     const int64_t E = env->E;
     const int A = p.act_dim;
@@ -1027,15 +1459,27 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
 int sng_graph_launch(SngGraph *g, void *stream) {
     if (!g) return SNG_ERR_INVALID_ARGUMENT;
     SngEnv *env = g->env;
-    if (!g->with_reset && g->packed != env->p.packed)
-        return fail(env, SNG_ERR_STATE, "graph captured for days of the other RNG mode: recapture it after this reset");
+    if (!g->with_reset) {
+        // a steps-only graph steps the loaded day from t = 0 with the Params it was captured with
+        if (!(g->key == day_key(env->p)))
+            return fail(env, SNG_ERR_STATE,
+                        "graph captured for a day of another encoding (RNG mode, requested-SoC stream or replay): "
+                        "recapture it after this reset");
+        if (env->t != 0) return fail(env, SNG_ERR_STATE, "a steps-only graph starts at t = 0: reset first");
+        if (env->seed != env->p.seed) return fail(env, SNG_ERR_STATE, "seed changed since capture");
+    }
     HIP_TRY(env, hipSetDevice(env->device));
     // the graph's first reset must not redraw a device day that was reset but never stepped
-    if (g->with_reset && env->p.packed && env->t == 0) HIP_TRY(env, launch_bump_day(env->ds, (hipStream_t)stream));
-    HIP_TRY(env, hipGraphLaunch(g->exec, (hipStream_t)stream));
+    if (g->with_reset && env->p.packed && env->p.bump_day && env->t == 0)
+        HIP_TRY(env, launch_bump_day(env->ds, as_stream(stream)));
+    HIP_TRY(env, hipGraphLaunch(g->exec, as_stream(stream)));
     if (g->with_reset) {
         env->p.req_stream = env->p.req_enabled;
         env->p.packed = 1;
+        env->p.req_zero = 0;
+        env->p.bump_day = 1;
+        env->gen_mode = SNG_RNG_DEVICE;
+        env->gen_loaded = true;
     }
     env->t = env->p.T;
     env->day_finished = true;
@@ -1056,10 +1500,12 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     if (!device_rng_ok(env)) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
     HIP_TRY(env, hipSetDevice(env->device));
-    hipStream_t st = (hipStream_t)stream;
+    hipStream_t st = as_stream(stream);
     Params p = env->p;
     p.req_stream = p.req_enabled;
     p.packed = 1;
+    p.req_zero = 0;
+    p.bump_day = 1;
     if (p.req_stream) {
         int rc = ensure_req(env);
         if (rc) return rc;
@@ -1070,7 +1516,7 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
     std::vector<hipEvent_t> ev(2 * (size_t)T * days, nullptr);
     hipError_t e = hipSuccess;
-    if (env->p.packed && env->t == 0) e = launch_bump_day(env->ds, st);   // as in sng_reset
+    if (env->p.packed && env->p.bump_day && env->t == 0) e = launch_bump_day(env->ds, st);   // as in sng_reset
     for (auto &x : ev)
         if (e == hipSuccess) e = hipEventCreate(&x);
     for (int d = 0; e == hipSuccess && d < days; ++d) {
@@ -1087,6 +1533,10 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     if (e != hipSuccess) return hip_fail(env, e, "timed day");
     env->p.req_stream = p.req_stream;
     env->p.packed = 1;
+    env->p.req_zero = 0;
+    env->p.bump_day = 1;
+    env->gen_mode = SNG_RNG_DEVICE;
+    env->gen_loaded = true;
     env->t = T;
     env->day_finished = true;
     return SNG_OK;
@@ -1109,7 +1559,7 @@ int sng_host_generate_scenarios(const SngConfig *cfg, int64_t num_envs, uint64_t
         np_rng.seed_numpy((uint32_t)(seed + (uint64_t)i));
         py_rng.seed_python(seed + (uint64_t)i);
         for (int ep = 0; ep < episodes; ++ep) {
-            if (ep > 0) (void)py_rng.py_randint(0, 180);   // day-end draw, smart_nanogrid_environment.py:190
+            if (ep > 0) (void)py_rng.py_randint(0, 180);   // day-end draw, smart_nanogrid_environment.py:181
             const size_t k = (size_t)ep * num_envs + i;
             DayView d{soc + k * N * S, occupancy + k * N * S, capacity + k * N * S, requested_soc + k * N * S,
                       arrivals + k * N * max_vehicles, departures + k * N * max_vehicles, max_vehicles, S};
@@ -1118,6 +1568,17 @@ int sng_host_generate_scenarios(const SngConfig *cfg, int64_t num_envs, uint64_t
         }
     }
     if (overflow) return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "max_vehicles too small");
+    return SNG_OK;
+}
+
+int32_t sng_host_threads(void) { return host_threads(); }
+
+int sng_get_day_counter(SngEnv *env, uint64_t *out, void *stream) {
+    if (!env) return SNG_ERR_INVALID_ARGUMENT;
+    if (!out) return fail(env, SNG_ERR_INVALID_ARGUMENT, "sng_get_day_counter: null output");
+    HIP_TRY(env, hipSetDevice(env->device));
+    HIP_TRY(env, hipMemcpyAsync(out, env->ds.episode, sizeof(uint64_t), hipMemcpyDeviceToHost, as_stream(stream)));
+    HIP_TRY(env, hipStreamSynchronize(as_stream(stream)));
     return SNG_OK;
 }
 

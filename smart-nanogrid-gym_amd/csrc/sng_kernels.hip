@@ -19,6 +19,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "sng.h"
 #include "sng_layout.h"
@@ -267,7 +268,7 @@ __device__ __forceinline__ void copy_out(float *__restrict__ dst, const float *_
     }
 }
 
-// Observation header (smart_nanogrid_environment.py:199-240, central_management_system.py:53-60):
+// Observation header (smart_nanogrid_environment.py:190-231, central_management_system.py:53-60):
 // [solar(t), price(t), solar(t+1..t+3), price(t+1..t+3)] with PV, [price(t), price(t+1..t+3)] without.
 // irr / pn point at irr_norm[t] / price_norm[t] (the step kernel's LDS copy, or the tables);
 // fpv / fpr are the env's profile factors for t..t+3 (1.0 without stochastic profiles).
@@ -327,7 +328,7 @@ __device__ __forceinline__ double step_constant(const Tables *tb, int t, int i) 
                       : i < CST_PV ? tb->price_norm[t + i - CST_PN] : i == CST_PV ? tb->pv_power[t] : tb->price[t];
 }
 
-// Remaining time to departure / 24 (smart_nanogrid_environment.py:216-217) as float32.
+// Remaining time to departure / 24 (smart_nanogrid_environment.py:207-208) as float32.
 // The reference rounds d / 24 in float64 and then to float32; for integers d < 256 that equals the
 // correctly rounded float32 quotient (d/24 is never a float32 rounding midpoint), which
 // q = d*r; q + fma(-q, 24, d)*r reproduces for every d < 256 (checked exhaustively).
@@ -425,8 +426,8 @@ __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t 
 
 // ---------------------------------------------------------------------------------
 // Env tail: BESS, grid energy, cost, reward (central_management_system.py:99-185,
-// battery_energy_storage_system.py:186-262, penaliser.py:104-111/177-187,
-// accountant.py:213-227) and the observation header.  Leader lane only.
+// battery_energy_storage_system.py:30-106, penaliser.py:104-111/177-187,
+// accountant.py:26-40) and the observation header.  Leader lane only.
 // ---------------------------------------------------------------------------------
 template <bool DIAG>
 __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, const InfoPtrs &info, int64_t e0, uint32_t lo, uint32_t el1, uint32_t el8,
@@ -446,8 +447,8 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
             bst(s.bess0, el8, bess);
             bess0 = bess;
         }
-        // charge (ba > 0, battery_energy_storage_system.py:186-218) and discharge (ba < 0,
-        // :220-262) share one select-based path with one division: the two branches differ only
+        // charge (ba > 0, battery_energy_storage_system.py:46-74) and discharge (ba < 0,
+        // :76-106) share one select-based path with one division: the two branches differ only
         // in their constants, the over-discharge clamp and the SoC bound
         const double ba = (double)bess_action;
         const bool chg = ba > 0.0;
@@ -649,15 +650,18 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         }
     };
     auto load_req = [&](int c0) {
-        if (p.req_stream) {
+        if (p.req_stream && !p.req_zero) {
 #pragma unroll
             for (int j = 0; j < CH; ++j) {
                 const int c = c0 + j;
                 req[j] = (c < cend) ? bld(req_t, el8, (uint32_t)c * (uint32_t)E * 8u) : 1.0;
             }
         } else {
+            // no stream: 1.0 (requested SoC disabled, charging_station.py:230-232); a replayed day: the
+            // cleared 0.0 (sng_layout.h, Params::req_zero)
+            const double rq = p.req_zero ? 0.0 : 1.0;
 #pragma unroll
-            for (int j = 0; j < CH; ++j) req[j] = 1.0;
+            for (int j = 0; j < CH; ++j) req[j] = rq;
         }
     };
     auto load_batch = [&](int c0) {
@@ -853,18 +857,58 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     SNG_STAMP(2);
     copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
     // a device-RNG day's first step advances the day counter its reset read (generate_kernel);
-    // nothing in this launch reads it (done last: at the top it perturbed the prologue's schedule)
-    if (PK && t == 0 && blockIdx.x == 0 && threadIdx.x == 0) *s.episode += 1;
+    // nothing in this launch reads it (done last: at the top it perturbed the prologue's schedule).
+    // A replayed day (bump_day = 0) drew no counter value of its own.
+    if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0) *s.episode += 1;
     SNG_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------------
+// Counter-based draws shared by the device generator and the t = 0 observation kernels: draw i
+// of a stream is mix32(key + i * golden), three 32-bit multiplies (the earlier 64-bit SplitMix
+// streams cost ~4x the VALU; the generator is bound by its dense timeline stores otherwise).
+// ---------------------------------------------------------------------------------
+struct HashStream {
+    uint32_t key, ctr;
+#ifdef SNG_GEN_CHEAP   // diagnostic build only: no hashing (timing floor of the generator's stores)
+    __device__ __forceinline__ uint32_t next() { return key ^ ((ctr++) * 0x9e3779b9u); }
+#else
+    __device__ __forceinline__ uint32_t next() { return mix32(key + (ctr++) * 0x9e3779b9u); }
+#endif
+};
+
+__device__ __forceinline__ double u32_unit(uint32_t x) { return (double)x * 0x1.0p-32; }   // [0, 1)
+
+__device__ __forceinline__ int below(uint32_t x, int n) {   // floor(x * n / 2^32)
+    return (int)(((uint64_t)x * (uint64_t)n) >> 32);
+}
+
+constexpr uint32_t kDomainRatio = 0x7a710000u;    // a generated day's PV ratio
+constexpr uint32_t kDomainReplay = 0x7a720000u;   // the PV ratio of a replayed day
+
+// random.randint(0, 180) / 100 (smart_nanogrid_environment.py:349) of device day `day`
+__device__ __forceinline__ double pv_ratio_draw(uint64_t seed, uint64_t ge, uint64_t day) {
+    HashStream r2{stream_key(seed, ge, kDomainRatio, day), 0u};
+    return (double)below(r2.next(), 181) / 100;
+}
+
+// The ratio a replayed device day redraws (reset(generate_new_initial_values=False) redraws
+// random_pv_shift_ratio, smart_nanogrid_environment.py:347-349): replay number `replay` of the handle.
+__device__ __forceinline__ double replay_ratio_draw(uint64_t seed, uint64_t ge, uint64_t replay) {
+    HashStream r2{stream_key(seed, ge, kDomainReplay, replay), 0u};
+    return (double)below(r2.next(), 181) / 100;
+}
+
+// ---------------------------------------------------------------------------------
 // Observation at t = 0 after a reset (SmartNanogridEnv.reset -> __get_observations,
-// smart_nanogrid_environment.py:358-360): SOC[c, 0] as generated, departure times at 0.
+// smart_nanogrid_environment.py:349-351): SOC[c, 0] as generated, departure times at 0.
+// mode (Obs0Mode, sng_layout.h) says where the PV ratio comes from and who advances the day
+// counter; replay = the handle's replay number (OBS0_REPLAY of a device day), else -1.
 // ---------------------------------------------------------------------------------
 template <int BLOCK, bool PK>
 __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s, float *__restrict__ obs,
-                                                         double *__restrict__ ep_return, int64_t E, int vec_io) {
+                                                         double *__restrict__ ep_return, int64_t E, int vec_io,
+                                                         int mode, int64_t replay) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int n = p.n, O = p.obs_dim;
     const int tid = threadIdx.x;
@@ -873,7 +917,19 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
     const int64_t e = e0 + tid;
     float *o_row = lds + tid * O;
     if (tid < nblk) {
-        const double ratio = s.ratio[e];
+        const uint64_t ge = (uint64_t)(e + p.env_offset);
+        double ratio;
+        if (mode == OBS0_DEVICE) {   // the day's draw, as the fused generator's t = 0 blocks make it
+            ratio = pv_ratio_draw(p.seed, ge, *s.episode);
+            s.ratio[e] = ratio;
+        } else if (mode == OBS0_REPLAY && replay >= 0) {
+            ratio = replay_ratio_draw(p.seed, ge, (uint64_t)replay);
+            s.ratio[e] = ratio;
+        } else {
+            ratio = s.ratio[e];
+        }
+        // a generated day's python index -1 slot holds zeros; a replayed day's Requested_SOC is 0
+        if (mode != OBS0_HOST) s.pen0[e] = 0.0;
         double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
         if (p.noise) {
             const size_t plane = (size_t)(p.T + 3) * E;
@@ -917,7 +973,9 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
         if (p.bess) o_row[O - 1] = (float)s.bess[e];
         if (ep_return) ep_return[e] = 0.0;
     }
-    if (blockIdx.x == 0 && tid == 0) *s.episode += 1;   // next device-RNG day
+    // a host day: profile_kernel read the counter for this day's factors, so the next day draws the
+    // next value (a device day's counter is advanced by its first step; a replay keeps its day's)
+    if (mode == OBS0_HOST && blockIdx.x == 0 && tid == 0) *s.episode += 1;
     __syncthreads();
     copy_out<BLOCK>(obs + e0 * O, lds, nblk * O, vec_io != 0, tid);
 }
@@ -945,26 +1003,9 @@ __global__ __launch_bounds__(256) void profile_kernel(Params p, DeviceState s, i
 // Device RNG day generator: the reference's per-charger vehicle process
 // (charging_station.py:200-279: arrival with p = 0.4 when the charger is free, arrival SoC
 // U(0.1, 0.9), capacity U{15..119}, requested SoC, departure U{t+4/dt .. min(t+10/dt, T+1/dt)-1})
-// with counter-based 32-bit hash streams, one per (global env, charger, day): draw i of a
-// stream is mix32(key + i * golden), three 32-bit multiplies (the earlier 64-bit SplitMix
-// streams cost ~4x the VALU; the kernel is bound by its dense timeline stores otherwise).
+// with counter-based 32-bit hash streams (HashStream), one per (global env, charger, day).
 // Thread = (env, charger); writes the dense packed-record (/ req) timeline.
 // ---------------------------------------------------------------------------------
-struct HashStream {
-    uint32_t key, ctr;
-#ifdef SNG_GEN_CHEAP   // diagnostic build only: no hashing (timing floor of the generator's stores)
-    __device__ __forceinline__ uint32_t next() { return key ^ ((ctr++) * 0x9e3779b9u); }
-#else
-    __device__ __forceinline__ uint32_t next() { return mix32(key + (ctr++) * 0x9e3779b9u); }
-#endif
-};
-
-__device__ __forceinline__ double u32_unit(uint32_t x) { return (double)x * 0x1.0p-32; }   // [0, 1)
-
-__device__ __forceinline__ int below(uint32_t x, int n) {   // floor(x * n / 2^32)
-    return (int)(((uint64_t)x * (uint64_t)n) >> 32);
-}
-
 // An arrival happens iff round(rand() - 0.1) == 1, i.e. rand() > 0.6 (p = 0.4) at each free step.
 
 constexpr int kGenBlock = 256;       // 4 waves of consecutive envs, same charger
@@ -1006,15 +1047,10 @@ __device__ __forceinline__ VehicleDraw draw_vehicle(const Params &p, HashStream 
     return d;
 }
 
-__device__ __forceinline__ double pv_ratio_draw(uint64_t seed, uint64_t ge, uint64_t day) {
-    HashStream r2{stream_key(seed, ge, 0x7a710000u, day), 0u};   // the PV-ratio domain
-    return (double)below(r2.next(), 181) / 100;                   // random.randint(0, 180) / 100
-}
-
 // The t = 0 observation of a device-RNG day, computed from the streams rather than read back from
 // the timeline, so it runs as extra blocks of the generator's grid with no dependency on the
 // timeline blocks (SmartNanogridEnv.reset -> __get_observations, smart_nanogrid_environment.py:
-// 358-360): each charger's first vehicle, if it arrives at t = 0, gives SOC[c, 0] and the
+// 349-351): each charger's first vehicle, if it arrives at t = 0, gives SOC[c, 0] and the
 // departure entry; the PV ratio, the day's profile factors, the header and the BESS entry; the
 // running SoC is seeded and the day return zeroed.  Thread = env; rows leave through LDS.
 __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4,
@@ -1108,7 +1144,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
             s_req[v * kGenBlock + tid] = lo + (1.0 - lo) * u32_unit(d.req_draw);
         }
         nv = v + 1;
-        tfree = d.dep + 1;   // the departure step stays empty (charging_station.py:247-255)
+        tfree = d.dep + 1;   // the departure step stays empty (charging_station.py:239-251)
     }
 
     // slot nv: a sentinel that never arrives (arrival = departure = 255), so phase 2 walks the
@@ -1223,40 +1259,59 @@ int step_lanes_supported(int n, int lanes) {
     return (lanes == 1 || (multi && (lanes == 2 || lanes == 4))) ? 1 : 0;
 }
 
+// The step kernel writes the diagnostics (DIAG) when any SngInfo array other than the flags and the
+// day return is given.
+static bool info_diag(const InfoPtrs &info) {
+    return info.grid_power || info.p_charge || info.p_discharge || info.bess_soc || info.pen_vehicle ||
+           info.pen_battery || info.grid_cost || info.total_cost || info.solar || info.bess_power ||
+           info.bess_calc_power || info.nonexistent || info.bess_initial || info.charger_power || info.vehicle_soc;
+}
+
 hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
                        double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
                        hipEvent_t ev_start, hipEvent_t ev_stop) {
     LaunchEvents evs{ev_start, ev_stop};
     const LaunchEvents *ev = (ev_start && ev_stop) ? &evs : nullptr;
-    const bool diag = info.grid_power || info.p_charge || info.p_discharge || info.bess_soc || info.pen_vehicle ||
-                      info.pen_battery || info.grid_cost || info.total_cost || info.solar || info.bess_power ||
-                      info.bess_calc_power || info.nonexistent || info.bess_initial || info.charger_power ||
-                      info.vehicle_soc;
-    if (diag)
+    if (info_diag(info))
         launch_step_n<true>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev);
     else
         launch_step_n<false>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev);
     return hipGetLastError();
 }
 
+// The name rocprofv3 reports for the step kernel launch_step would dispatch next (the template
+// arguments launch_step_n / launch_step_l / launch_step_t select).
+int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) {
+    int nc = 0, lanes = 1;
+    switch (p.n) {
+        case 2: case 4: case 8: case 10: case 16: case 50:
+            nc = p.n;
+            lanes = (p.lanes == 2 || p.lanes == 4) ? p.lanes : 1;
+            break;
+        case 1: nc = 1; break;
+        default: nc = 0; break;
+    }
+    const bool fast = !p.legacy && p.dt_pow2;
+    return snprintf(buf, (size_t)len, "void sng::step_kernel<%d, %d, %s, %s, %s>", nc, lanes,
+                    info_diag(info) ? "true" : "false", fast ? "true" : "false", p.packed ? "true" : "false");
+}
+
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
-                           int vec_io, hipStream_t stream) {
+                           int vec_io, hipStream_t stream, int mode, int64_t replay) {
     if ((size_t)round4(256 * p.obs_dim) * 4 <= 64 * 1024) {
         const dim3 grid((unsigned)((E + 255) / 256)), block(256);
         auto kern = p.packed ? observe0_kernel<256, true> : observe0_kernel<256, false>;
         hipLaunchKernelGGL(kern, grid, block, (size_t)round4(256 * p.obs_dim) * 4, stream, p, s, obs, ep_return, E,
-                           vec_io);
+                           vec_io, mode, replay);
     } else {
         const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
         auto kern = p.packed ? observe0_kernel<kWave, true> : observe0_kernel<kWave, false>;
         hipLaunchKernelGGL(kern, grid, block, (size_t)round4(kWave * p.obs_dim) * 4, stream, p, s, obs, ep_return, E,
-                           vec_io);
+                           vec_io, mode, replay);
     }
     return hipGetLastError();
 }
 
-hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
-                           int vec_io, hipStream_t stream);
 hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream);
 
 // A whole device-RNG reset.  The t = 0 observation runs as extra blocks of the generator's grid
@@ -1273,7 +1328,8 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
     if (fused) return hipGetLastError();
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = launch_profiles(p, s, E, stream);
-    if (e == hipSuccess) e = launch_observe0(p, s, obs, ep_return, E, vec_io, stream);
+    // the PV ratio and pen0 of the day, from the streams, as the fused t = 0 blocks do
+    if (e == hipSuccess) e = launch_observe0(p, s, obs, ep_return, E, vec_io, stream, OBS0_DEVICE, -1);
     return e;
 }
 

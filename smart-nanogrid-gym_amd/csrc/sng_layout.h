@@ -49,7 +49,7 @@ constexpr int W_DEP_SHIFT = 16;
 constexpr int kMaxChargers = 128;   // numpy pairwise sum restated for n <= 128 (single level)
 constexpr int kSlots = 25;          // charger.py:16-19
 constexpr int kMaxT = 128;
-constexpr int kPriceLen = 48;       // accountant.py:201, 236 (2T with the extended day)
+constexpr int kPriceLen = 48;       // accountant.py:14, 49 (2T with the extended day)
 
 SNG_HD inline uint32_t pack_word(bool occ, bool stat, bool pen, uint32_t cap, uint32_t dep) {
     return (occ ? W_OCC : 0u) | (stat ? W_STATIC : 0u) | (pen ? W_PEN : 0u) | ((cap & 0xffu) << W_CAP_SHIFT) |
@@ -58,10 +58,10 @@ SNG_HD inline uint32_t pack_word(bool occ, bool stat, bool pen, uint32_t cap, ui
 
 // Constant tables, in device memory, read with scalar (wave-uniform) loads.
 struct Tables {
-    double irr_norm[4 * kMaxT];    // irr[k] / irr_max          (pv_system_manager.py:369-373)
-    double pv_power[4 * kMaxT];    // available_solar_power[k]  (:375-379)
-    double price[4 * kMaxT];       // energy_price[0, k]        (accountant.py:225-227)
-    double price_norm[4 * kMaxT];  // energy_price / max        (:229-233)
+    double irr_norm[4 * kMaxT];    // irr[k] / irr_max          (pv_system_manager.py:81-85)
+    double pv_power[4 * kMaxT];    // available_solar_power[k]  (:87-91)
+    double price[4 * kMaxT];       // energy_price[0, k]        (accountant.py:38-40)
+    double price_norm[4 * kMaxT];  // energy_price / max        (:42-46)
     double recip[256];             // 1.0 / c (correctly rounded), c = vehicle capacity; recip[0] = 0
     int32_t n_irr;
 };
@@ -85,6 +85,11 @@ struct Params {
     int32_t lanes;            // step kernel: lanes per environment (1, 2 or 4)
     int32_t noise;            // 1: stochastic PV / price profiles (DeviceState::prof is live)
     int32_t packed;           // 1: the day's timeline is packed records in `aux` (device-RNG days)
+    int32_t req_zero;         // 1: Requested_SOC is 0 on every slot -- a replayed day: load_initial_values
+                              //    (charging_station.py:119-136) does not restore what clear_initialisation_
+                              //    variables (:138-150) zeroed, so no vehicle is ever insufficiently charged
+    int32_t bump_day;         // 1: the loaded device-RNG day owns a day-counter value, which its first step
+                              //    advances (0 for a replayed day: its counter value was advanced already)
     double pv_noise, price_noise;
     uint64_t seed;            // handle seed: env e's seed is seed + env_offset + e
 };
@@ -98,6 +103,17 @@ struct DeviceState {
     double *prof;
     uint64_t *episode;        // device-side day counter for the device generator
     const Tables *tables;
+};
+
+// What observe0_kernel (the t = 0 observation of a day the fused generator did not write) does with
+// the PV ratio, the t = 0 penalty and the day counter.
+enum Obs0Mode : int32_t {
+    OBS0_HOST = 0,     // host-RNG or injected day: ratio and pen0 were uploaded; advances the day counter
+                       // (profile_kernel read it for this day's profile factors)
+    OBS0_DEVICE = 1,   // device-RNG day of a wide station (generator launched without its t = 0 blocks):
+                       // ratio drawn from the day's stream, pen0 = 0; the day's first step advances the counter
+    OBS0_REPLAY = 2,   // replayed day, reset(generate_new_initial_values=False): pen0 = 0, counter untouched;
+                       // ratio uploaded (reference RNG) or drawn from the replay stream (device RNG)
 };
 
 struct InfoPtrs {

@@ -3,7 +3,7 @@
 //   numpy legacy RandomState (np.random.seed / rand / uniform / randint), used by
 //     ChargingStation.generate_initial_vehicle_presence_per_charger (charging_station.py:200-279)
 //   Python `random` (random.seed / randint), used for random_pv_shift_ratio
-//     (smart_nanogrid_environment.py:190, 358)
+//     (smart_nanogrid_environment.py:181, 349)
 #pragma once
 #include <stdint.h>
 
@@ -77,6 +77,19 @@ class MT19937 {
             r = next() >> (32 - k);
         } while (r >= n);
         return a + (int64_t)r;
+    }
+
+    // checkpoint / resume (sng_get_state): the 624 state words and the position
+    static constexpr int kStateWords = N + 1;
+    void save(uint32_t *out) const {
+        for (int i = 0; i < N; ++i) out[i] = mt_[i];
+        out[N] = (uint32_t)mti_;
+    }
+    bool load(const uint32_t *in) {
+        if (in[N] > (uint32_t)N + 1) return false;
+        for (int i = 0; i < N; ++i) mt_[i] = in[i];
+        mti_ = (int)in[N];
+        return true;
     }
 
    private:

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SNG_LIBRARY", os.path.join(os.path.dirname(PKG_DIR), 
 DATA_DIR = os.path.join(PKG_DIR, "data")
 IRRADIANCE_FILE = os.path.join(DATA_DIR, "solar_irradiance_1min.f64")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 SNG_OK = 0
 RNG_REFERENCE = 0
 RNG_DEVICE = 1
@@ -95,41 +95,50 @@ class SngScenario(ctypes.Structure):
                 ("pv_ratio", c_double_p)]
 
 
+_H, _S = ctypes.c_void_p, ctypes.c_void_p   # handle, hipStream_t
 EXPORTS = {
     "sng_abi_version": (ctypes.c_int32, []),
     "sng_config_defaults": (None, [ctypes.POINTER(SngConfig)]),
     "sng_create": (ctypes.c_int, [ctypes.POINTER(SngConfig), ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
                                   ctypes.POINTER(ctypes.c_void_p)]),
-    "sng_destroy": (None, [ctypes.c_void_p]),
-    "sng_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
-    "sng_get_dims": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SngDims)]),
-    "sng_get_timestep": (ctypes.c_int, [ctypes.c_void_p]),
-    "sng_set_env_offset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
-    "sng_reset": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
-    "sng_reset_from_scenario": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(SngScenario), ctypes.c_void_p,
-                                               ctypes.c_void_p]),
-    "sng_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                ctypes.c_void_p, ctypes.POINTER(SngInfo), ctypes.c_void_p]),
-    "sng_read_errors": (ctypes.c_int, [ctypes.c_void_p, c_uint32_p, ctypes.c_int]),
-    "sng_get_battery_soc": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
-    "sng_set_battery_soc": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
-    "sng_get_pv_ratio": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
-    "sng_get_vehicle_soc": (ctypes.c_int, [ctypes.c_void_p, c_double_p]),
-    "sng_get_scenario": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, c_double_p, c_double_p,
-                                        c_double_p, c_double_p, c_int32_p, c_int32_p, c_int32_p, c_double_p]),
-    "sng_get_tables": (ctypes.c_int, [ctypes.c_void_p, c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
+    "sng_destroy": (None, [_H]),
+    "sng_last_error": (ctypes.c_char_p, [_H]),
+    "sng_get_dims": (ctypes.c_int, [_H, ctypes.POINTER(SngDims)]),
+    "sng_get_timestep": (ctypes.c_int, [_H]),
+    "sng_set_env_offset": (ctypes.c_int, [_H, ctypes.c_int64]),
+    "sng_set_seed": (ctypes.c_int, [_H, ctypes.c_uint64, _S]),
+    "sng_reset": (ctypes.c_int, [_H, ctypes.c_int, ctypes.c_void_p, _S]),
+    "sng_reset_replay": (ctypes.c_int, [_H, ctypes.c_void_p, _S]),
+    "sng_reset_from_scenario": (ctypes.c_int, [_H, ctypes.POINTER(SngScenario), ctypes.c_void_p, _S]),
+    "sng_step": (ctypes.c_int, [_H, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                ctypes.c_void_p, ctypes.POINTER(SngInfo), _S]),
+    "sng_step_kernel_name": (ctypes.c_int, [_H, ctypes.POINTER(SngInfo), ctypes.c_char_p, ctypes.c_int32]),
+    "sng_read_errors": (ctypes.c_int, [_H, c_uint32_p, ctypes.c_int, _S]),
+    "sng_get_battery_soc": (ctypes.c_int, [_H, c_double_p, _S]),
+    "sng_set_battery_soc": (ctypes.c_int, [_H, c_double_p, _S]),
+    "sng_get_pv_ratio": (ctypes.c_int, [_H, c_double_p, _S]),
+    "sng_get_vehicle_soc": (ctypes.c_int, [_H, c_double_p, _S]),
+    "sng_set_vehicle_soc": (ctypes.c_int, [_H, c_double_p, _S]),
+    "sng_state_size": (ctypes.c_int, [_H, ctypes.c_int, ctypes.POINTER(ctypes.c_size_t)]),
+    "sng_get_state": (ctypes.c_int, [_H, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, _S]),
+    "sng_set_state": (ctypes.c_int, [_H, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, _S]),
+    "sng_get_scenario": (ctypes.c_int, [_H, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32, c_double_p, c_double_p,
+                                        c_double_p, c_double_p, c_int32_p, c_int32_p, c_int32_p, c_double_p, _S]),
+    "sng_get_tables": (ctypes.c_int, [_H, c_double_p, c_double_p, c_double_p, c_double_p, c_double_p,
                                       c_int32_p]),
-    "sng_graph_create": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+    "sng_graph_create": (ctypes.c_int, [_H, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.POINTER(SngInfo), ctypes.c_int, ctypes.c_int32,
                                         ctypes.c_void_p, ctypes.POINTER(ctypes.c_void_p)]),
-    "sng_graph_launch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    "sng_graph_launch": (ctypes.c_int, [ctypes.c_void_p, _S]),
     "sng_graph_destroy": (None, [ctypes.c_void_p]),
-    "sng_time_step_kernels": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+    "sng_time_step_kernels": (ctypes.c_int, [_H, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.POINTER(SngInfo), ctypes.c_int32, c_float_p,
-                                             ctypes.c_void_p]),
+                                             _S]),
     "sng_host_generate_scenarios": (ctypes.c_int, [ctypes.POINTER(SngConfig), ctypes.c_int64, ctypes.c_uint64,
                                                    ctypes.c_int32, c_double_p, c_double_p, c_double_p, c_double_p,
                                                    c_int32_p, c_int32_p, ctypes.c_int32, c_double_p]),
+    "sng_host_threads": (ctypes.c_int32, []),
+    "sng_get_day_counter": (ctypes.c_int, [_H, ctypes.POINTER(ctypes.c_uint64), _S]),
 }
 
 _lib = None

@@ -51,8 +51,10 @@ class SmartNanogridEnv(_Base):
         self.recorder = DayRecorder(self._venv, [0], results_directory) if results_directory is not None else None
 
     def reset(self, generate_new_initial_values=True, algorithm_used="", environment_mode="", **kwargs):
-        """smart_nanogrid_environment.py:320-360 (gym-0.26 `seed=`/`options=` are accepted and ignored,
-        as the reference swallows them in **kwargs)."""
+        """smart_nanogrid_environment.py:311-351 (gym-0.26 `seed=`/`options=` are accepted and ignored,
+        as the reference swallows them in **kwargs).  generate_new_initial_values=False replays the last
+        generated day with Requested_SOC cleared and a new PV ratio, as the reference's load_initial_values
+        does (charging_station.py:119-136; what solvers/evaluator.py:88-101 relies on)."""
         obs = self._venv.reset(generate_new_initial_values, algorithm_used, environment_mode,
                                **{k: v for k, v in kwargs.items() if k not in ("seed", "options")})
         self.simulated_single_day = False
@@ -60,7 +62,7 @@ class SmartNanogridEnv(_Base):
         return obs[0], {}
 
     def step(self, actions):
-        """smart_nanogrid_environment.py:149-197.  After the day ends call reset() (the reference would
+        """smart_nanogrid_environment.py:140-188.  After the day ends call reset() (the reference would
         silently re-run the day on its mutated arrays; this raises instead)."""
         if self.simulated_single_day:
             raise RuntimeError("the simulated day is over: call reset()")
@@ -79,6 +81,11 @@ class SmartNanogridEnv(_Base):
         self.timestep = 0 if terminated else self.timestep + 1
         self.simulated_single_day = terminated
         return v._obs_h.numpy()[0].copy(), np.float64(v._rew_h.numpy()[0]), terminated, False, {}
+
+    @property
+    def random_pv_shift_ratio(self):
+        """The day's PV shift ratio (smart_nanogrid_environment.py:65, :181, :349)."""
+        return float(self._venv.pv_ratio()[0])
 
     def render(self, mode="human"):
         pass

@@ -19,8 +19,11 @@ Differences from the reference scripts (deliberate, documented):
   * Every (model, episode) slot starts the day with the same battery state of charge
     (`battery_initial_soc`, default the config's); the reference's evaluator shares ONE env per
     variant, so each model's episode inherits the battery its predecessor left.
-  * Replayed days keep the generating day's PV shift ratio.  The reference redraws it from the
-    global `random` stream at every reset, replays included (smart_nanogrid_environment.py:349).
+  * Replayed days keep the generating day's PV shift ratio and requested SoC.  The reference redraws
+    the ratio from the global `random` stream at every reset, replays included
+    (smart_nanogrid_environment.py:349), and its replays leave Requested_SOC at 0
+    (charging_station.py:119-136).  The unchanged single-env loop above reproduces that exactly:
+    SmartNanogridEnv.reset(generate_new_initial_values=False) replays the env's last generated day.
 """
 import numpy as np
 
@@ -133,10 +136,10 @@ def generate_days(episodes, *, seed=0, device=0, rng="reference", **env_kwargs):
     try:
         gen.reset_tensors()
         torch.cuda.current_stream(gen.device).synchronize()
-        days = [gen.get_scenario(i) for i in range(episodes)]
+        ivs, ratios = gen.get_scenarios(0, episodes)
     finally:
         gen.close()
-    return [d for d, _ in days], np.array([r for _, r in days])
+    return ivs, ratios
 
 
 def evaluate_models(models, episodes=100, *, seed=0, device=0, rng="reference", battery_initial_soc=None,

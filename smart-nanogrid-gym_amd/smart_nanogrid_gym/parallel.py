@@ -21,18 +21,36 @@ def shard_envs(total_envs, world_size, rank):
     return offset, count
 
 
+def _fused_gather(group=None):
+    """all_gather_into_tensor on RCCL/NCCL; the list form elsewhere (gloo).  Chosen from the backend, which
+    every rank of the group shares, so all ranks issue the same collective."""
+    return dist.get_backend(group) == "nccl"
+
+
+def check_equal_shards(count, device=None, group=None):
+    """The single-buffer gathers need the same number of envs on every rank (weak scaling); shard_envs
+    gives unequal counts when total % world != 0.  One all-reduce of (count, -count) tells every rank the
+    max and min, so every rank raises together instead of one rank entering a mismatched collective."""
+    t = torch.tensor([float(count), -float(count)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+    if t[0].item() != -t[1].item():
+        raise ValueError(f"env shards differ in size across ranks ({int(-t[1].item())}..{int(t[0].item())}): "
+                         "use a total divisible by the world size")
+
+
 def all_gather_returns(local, group=None):
     """Gather every rank's per-env returns into one [total_envs] tensor in global env order.
-    Shards must be equal-sized (weak scaling) for the single-buffer collective."""
+    Shards must be equal-sized (weak scaling); checked on every rank first."""
     world = dist.get_world_size(group)
-    out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
-    try:
-        dist.all_gather_into_tensor(out, local.contiguous(), group=group)
-    except (RuntimeError, NotImplementedError, AttributeError):   # backends without the fused form
-        parts = [torch.empty_like(local) for _ in range(world)]
-        dist.all_gather(parts, local.contiguous(), group=group)
-        out = torch.cat(parts)
-    return out
+    local = local.contiguous()
+    check_equal_shards(local.numel(), device=local.device, group=group)
+    if _fused_gather(group):
+        out = torch.empty(world * local.numel(), dtype=local.dtype, device=local.device)
+        dist.all_gather_into_tensor(out, local, group=group)
+        return out
+    parts = [torch.empty_like(local) for _ in range(world)]
+    dist.all_gather(parts, local, group=group)
+    return torch.cat(parts)
 
 
 class DayReturnExchange:
@@ -45,6 +63,8 @@ class DayReturnExchange:
     def __init__(self, days, envs, device, group=None):
         self.group = group
         self.world = dist.get_world_size(group)
+        check_equal_shards(envs, device=device, group=group)
+        self.fused = _fused_gather(group)
         self.snap = [torch.zeros((days, envs), dtype=torch.float64, device=device) for _ in range(2)]
         self.out = [torch.empty((self.world, days, envs), dtype=torch.float64, device=device) for _ in range(2)]
         self.work = [None, None]
@@ -59,9 +79,9 @@ class DayReturnExchange:
 
     def gather(self, k):
         """Start the all-gather of buffer k (after the replay that fills it has been launched)."""
-        try:
+        if self.fused:
             self.work[k] = dist.all_gather_into_tensor(self.out[k], self.snap[k], group=self.group, async_op=True)
-        except (RuntimeError, NotImplementedError, AttributeError):   # backends without the fused form
+        else:
             self.work[k] = dist.all_gather(list(self.out[k].unbind(0)), self.snap[k], group=self.group,
                                            async_op=True)
         self.gathers += 1

@@ -16,7 +16,8 @@ Differences from the reference, by design:
   - values are floats throughout (the reference writes an int 0 where a penalty list was
     empty); numerically identical;
   - for a day started from given arrays (reset_from_initial_values / reset_from_arrays) the
-    initial values written are that day's (the reference writes the last *generated* day's);
+    initial values written are that day's (the reference writes the last *generated* day's, as
+    this recorder does for a replayed day);
   - with stochastic PV profiles (pv_noise > 0, not in the reference) 'Available_solar_energy'
     is the noise-free table.
 """
@@ -81,7 +82,11 @@ class DayRecorder:
 
     # ------------------------------------------------------------------ hooks (called by the env)
     def day_started(self):
-        self._initial = {i: self.venv.get_scenario(i)[0] for i in self.env_ids}
+        # a replayed day (reset(generate_new_initial_values=False)) writes the initial values of the last
+        # generated day, as the reference's save_initial_values_to_json_file writes
+        # generated_initial_values_json (charging_station.py:182-191), which load_initial_values leaves alone
+        if not (self.venv._last_reset == "replay" and all(i in self._initial for i in self.env_ids)):
+            self._initial = {i: self.venv.get_scenario(i)[0] for i in self.env_ids}
         self._steps = {i: [] for i in self.env_ids}
         self._started = True
 
@@ -114,7 +119,7 @@ class DayRecorder:
         dt = st.time_interval
         w_b = st.constants.get("battery_penalty_weight", 0.8)
         initial_soc = self._initial[env_index]["SOC"]
-        # SOC[c, t] is rewritten by step t (charger.py:36-53); slots no step reached keep their values
+        # SOC[c, t] is rewritten by step t (charger.py:37-56); slots no step reached keep their values
         soc = [[float(steps[t]["vehicle_soc"][c]) if t < len(steps) else initial_soc[c][t] for t in range(S)]
                for c in range(N)]
         col = lambda f: [s[f] for s in steps]   # noqa: E731
@@ -128,7 +133,7 @@ class DayRecorder:
         out = {
             "SOC": soc,
             "Grid_power": col("grid_power"),
-            "Grid_energy": [g * dt for g in col("grid_power")],                    # :103
+            "Grid_energy": [g * dt for g in col("grid_power")],   # central_management_system.py:107
             "Utilized_solar_energy": col("utilized_solar_energy"),
             "Total_vehicle_penalties": pen_v,
             "Total_battery_penalties": pen_b,
@@ -144,11 +149,11 @@ class DayRecorder:
             "Total_discharging_power": col("total_discharging_power"),
             "Charger_power_values": [s["charger_power"].tolist() for s in steps],
             "Battery_power_value": col("battery_power_value"),
-            "Battery_SOC_below_DoD_penalties": pen_b,                             # penaliser.py:184-185
+            "Battery_SOC_below_DoD_penalties": pen_b,                             # penaliser.py:183-184
             "Low_resource_utilisation_penalties": zeros,                          # never computed
             "Battery_overcharging_penalties": zeros,
             "Battery_over_discharging_penalties": zeros,
-            "Insufficiently_charged_vehicle_penalties": pen_v,                    # penaliser.py:187-188
+            "Insufficiently_charged_vehicle_penalties": pen_v,                    # penaliser.py:186-187
             "Needlessly_charged_vehicle_penalties": zeros,
             "Overcharged_vehicle_penalties": zeros,
             "Over_discharged_vehicle_penalties": zeros,

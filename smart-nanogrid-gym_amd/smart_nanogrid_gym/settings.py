@@ -1,7 +1,7 @@
 """Constructor keyword arguments of the reference env -> SngConfig.
 
 Same names, defaults and parsing as SmartNanogridEnv.__init__ / set_time_interval
-(smart_nanogrid_environment.py:41-147); the reference's hard-coded module constants
+(smart_nanogrid_environment.py:32-138); the reference's hard-coded module constants
 (BESS, EV, tariffs, penalty weights) become overridable fields with the reference values.
 """
 import ctypes
@@ -12,12 +12,12 @@ PENALTY_MODES = {"no_penalty": 0, "on_departure": 1, "sparse": 2, "dense": 3}
 
 WRONG_PENALTY_MODE = "Error: Wrong vehicle uncharged - penalty mode provided!"   # charging_station.py:60
 WRONG_CHARGING_MODE = "Error: Wrong charging mode provided!"                     # charger.py:88
-NEGATIVE_DEMAND = "Error: If V2X mode is not enabled, then power_demand cannot be less than 0!"  # cms.py:159
+NEGATIVE_DEMAND = "Error: If V2X mode is not enabled, then power_demand cannot be less than 0!"  # central_management_system.py:159
 BESS_ABOVE_ONE = "Error: Battery SOC greater than 1!"                              # penaliser.py:111
 
 
 def parse_time_interval(requested_time_interval):
-    """set_time_interval (smart_nanogrid_environment.py:134-147): '1h' -> 1.0, '15min' -> 0.25, '' -> 1.0."""
+    """set_time_interval (smart_nanogrid_environment.py:125-138): '1h' -> 1.0, '15min' -> 0.25, '' -> 1.0."""
     if requested_time_interval:
         if "h" in requested_time_interval:
             return float(requested_time_interval.replace("h", ""))
@@ -34,7 +34,7 @@ class EnvSettings:
                  algorithm_used="", environment_mode="", time_interval="", charging_mode="",
                  vehicle_uncharged_penalty_mode="", numpy_legacy_promotion=False, grid_cost_weight=0.75,
                  **constants):
-        if price_model == 5:   # accountant.py:277-278 indexes a list with a tuple
+        if price_model == 5:   # accountant.py:90-98 indexes a list with a tuple
             raise TypeError("list indices must be integers or slices, not tuple")
         if price_model not in (0, 1, 2, 3, 4):
             raise ValueError(f"unsupported price_model {price_model!r}")
@@ -86,7 +86,7 @@ class EnvSettings:
         return cfg
 
     def variant_name(self):
-        """smart_nanogrid_environment.py:289-296"""
+        """smart_nanogrid_environment.py:280-287"""
         if self.bess and self.pv and self.v2x:
             return "v2x-b-pv"
         if self.v2x:

@@ -1,4 +1,4 @@
-"""Observation/action spaces (smart_nanogrid_environment.py:99-129).
+"""Observation/action spaces (smart_nanogrid_environment.py:90-120).
 
 Uses gymnasium.spaces.Box or gym.spaces.Box when one of them is importable, so SB3
 sees the class it expects; otherwise a minimal Box with the same attributes.

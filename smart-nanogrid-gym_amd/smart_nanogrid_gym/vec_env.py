@@ -8,8 +8,9 @@ reset at the end of the day and the final observation in infos[i]['terminal_obse
 `reset_tensors` / `step_tensors` keep everything on the GPU for device-resident RL loops.
 
 Reference behaviour mirrored per env (smart_nanogrid_gym/envs/smart_nanogrid_environment.py):
-  reset()  -> new day, t = 0, BESS state of charge carried over (:320-360)
-  step(a)  -> (obs float32, reward = -total cost float64, terminated, truncated=False, {}) (:149-197)
+  reset()  -> new day, t = 0, BESS state of charge carried over (:311-351)
+  reset(generate_new_initial_values=False) -> the last generated day replayed (:347-357)
+  step(a)  -> (obs float32, reward = -total cost float64, terminated, truncated=False, {}) (:140-188)
   errors   -> the reference's ValueErrors, raised after the step that hit them
 """
 import ctypes
@@ -47,6 +48,7 @@ class SmartNanogridVecEnv:
     """
 
     metadata = {"render_modes": []}
+    render_mode = None
 
     def __init__(self, num_envs=1, *, seed=0, device=0, rng="reference", info=False, env_offset=0, **env_kwargs):
         if torch is None or not torch.cuda.is_available():
@@ -94,6 +96,7 @@ class SmartNanogridVecEnv:
         self._flags_h = torch.zeros(E, dtype=torch.int32, **pin)
         self._pending = None
         self._warned_breakpoint = False
+        self._last_reset = None   # 'generated', 'replay' or 'injected': how the loaded day began
         self.closed = False
 
     # ------------------------------------------------------------------ lifecycle
@@ -149,6 +152,24 @@ class SmartNanogridVecEnv:
             self.return_d.zero_()
             check(lib().sng_reset(self._h, mode, ctypes.c_void_p(self.obs_d.data_ptr()),
                                   _stream_handle(self.device)), self._h)
+        self._last_reset = "generated"
+        for r in self._recorders:
+            r.day_started()
+        return self.obs_d
+
+    def replay_tensors(self):
+        """reset(generate_new_initial_values=False) (smart_nanogrid_environment.py:347-357): every env replays
+        the day it last generated, as the reference's load_initial_values (charging_station.py:119-136)
+        re-reads the initial_values.json its generation wrote -- same vehicles, Requested_SOC cleared to 0
+        (so no vehicle penalty), a new PV ratio from the env's stream, BESS carried over.  Returns the t=0
+        observations (device tensor).  The reference's file is one per process; here each env replays its
+        own last generated day."""
+        self._check_mode()
+        with torch.cuda.device(self.device):
+            self.return_d.zero_()
+            check(lib().sng_reset_replay(self._h, ctypes.c_void_p(self.obs_d.data_ptr()),
+                                         _stream_handle(self.device)), self._h)
+        self._last_reset = "replay"
         for r in self._recorders:
             r.day_started()
         return self.obs_d
@@ -168,13 +189,18 @@ class SmartNanogridVecEnv:
             r.step_done(actions)
         return self.obs_d, self.reward_d, self.done_d
 
-    def reset_from_initial_values(self, initial_values, pv_ratio, restore_requested_soc=False):
-        """reset(generate_new_initial_values=False) (smart_nanogrid_environment.py:362-366).
+    def step_kernel_name(self):
+        """The step kernel the next step_tensors launches, as rocprofv3 names it (sng_step_kernel_name)."""
+        buf = ctypes.create_string_buffer(128)
+        check(lib().sng_step_kernel_name(self._h, ctypes.byref(self._info), buf, len(buf)), self._h)
+        return buf.value.decode()
 
-        initial_values: one dict (broadcast to all envs) or a list of num_envs dicts in the
-        reference's initial_values.json schema (charging_station.py:164-180).  The reference's
-        load_initial_values (charging_station.py:119-136) does not restore 'Requested_SOC'
-        (left at 0); restore_requested_soc=True uses the recorded values instead.
+    def reset_from_initial_values(self, initial_values, pv_ratio=None, restore_requested_soc=False):
+        """Start a day from the reference's initial_values.json dicts (charging_station.py:164-180): one
+        dict (broadcast to all envs) or a list of num_envs dicts.  The reference's load_initial_values
+        (charging_station.py:119-136) does not restore 'Requested_SOC' (left at 0);
+        restore_requested_soc=True uses the recorded values instead.  pv_ratio None: each env draws its
+        ratio from its Python stream (smart_nanogrid_environment.py:349), as a reset does.
         """
         self._check_mode()
         E, N = self.num_envs, self.settings.number_of_chargers
@@ -198,17 +224,17 @@ class SmartNanogridVecEnv:
             for c in range(N):
                 arr[i, c, :len(d["Arrivals"][c])] = d["Arrivals"][c]
                 dep[i, c, :len(d["Departures"][c])] = d["Departures"][c]
-        ratio = np.broadcast_to(np.asarray(pv_ratio, np.float64), (E,)).copy()
+        ratio = None if pv_ratio is None else np.broadcast_to(np.asarray(pv_ratio, np.float64), (E,)).copy()
         return self.reset_from_arrays(soc, occ, cap, req, arr, dep, ratio)
 
-    def reset_from_arrays(self, soc, occupancy, capacity, requested_soc, arrivals, departures, pv_ratio):
+    def reset_from_arrays(self, soc, occupancy, capacity, requested_soc, arrivals, departures, pv_ratio=None):
         """Start a day from explicit reference-layout arrays ([E, N, slots] / [E, N, V], -1 padded;
-        slots = 25, or T+1 with the build-defined extended day)."""
+        slots = 25, or T+1 with the build-defined extended day).  pv_ratio None: drawn per env from its
+        Python stream."""
         self._check_mode()
         arrs = [np.ascontiguousarray(a, np.float64) for a in (soc, occupancy, capacity, requested_soc)]
         ai = np.ascontiguousarray(arrivals, np.int32)
         di = np.ascontiguousarray(departures, np.int32)
-        ratio = np.ascontiguousarray(pv_ratio, np.float64)
         sc = _native.SngScenario()
         if arrs[0].shape[-1] != self.slots:
             raise ValueError(f"scenario arrays need {self.slots} slots per charger")
@@ -217,28 +243,34 @@ class SmartNanogridVecEnv:
         sc.soc, sc.occupancy, sc.capacity, sc.requested_soc = [a.ctypes.data_as(_native.c_double_p) for a in arrs]
         sc.arrivals = ai.ctypes.data_as(_native.c_int32_p)
         sc.departures = di.ctypes.data_as(_native.c_int32_p)
-        sc.pv_ratio = ratio.ctypes.data_as(_native.c_double_p)
+        if pv_ratio is not None:
+            ratio = np.ascontiguousarray(np.broadcast_to(np.asarray(pv_ratio, np.float64), (self.num_envs,)))
+            sc.pv_ratio = ratio.ctypes.data_as(_native.c_double_p)
         with torch.cuda.device(self.device):
             self.return_d.zero_()
             check(lib().sng_reset_from_scenario(self._h, ctypes.byref(sc), ctypes.c_void_p(self.obs_d.data_ptr()),
                                                 _stream_handle(self.device)), self._h)
             torch.cuda.current_stream(self.device).synchronize()
+        self._last_reset = "injected"
         for r in self._recorders:
             r.day_started()
         return self._obs_to_host()
 
     # ------------------------------------------------------------------ SB3 VecEnv API
     def reset(self, generate_new_initial_values=True, algorithm_used="", environment_mode="", **kwargs):
+        """smart_nanogrid_environment.py:311-351.  generate_new_initial_values=False replays the last
+        generated day (replay_tensors); with initial_values=<dict or list> (and optionally pv_ratio=,
+        restore_requested_soc=) it starts from those days instead (reset_from_initial_values)."""
         if algorithm_used:
             self.settings.algorithm_used = algorithm_used
         if environment_mode:
             self.settings.environment_mode = environment_mode
         if not generate_new_initial_values:
-            if "initial_values" not in kwargs:
-                raise ValueError("reset(generate_new_initial_values=False) needs initial_values=<dict> "
-                                 "(and pv_ratio=...) in this implementation")
-            return self.reset_from_initial_values(kwargs["initial_values"], kwargs.get("pv_ratio", 1.0),
-                                                  kwargs.get("restore_requested_soc", False))
+            if "initial_values" in kwargs:
+                return self.reset_from_initial_values(kwargs["initial_values"], kwargs.get("pv_ratio"),
+                                                      kwargs.get("restore_requested_soc", False))
+            self.replay_tensors()
+            return self._obs_to_host()
         self.reset_tensors()
         return self._obs_to_host()
 
@@ -281,20 +313,77 @@ class SmartNanogridVecEnv:
         return self.step_wait()
 
     def seed(self, seed=None):
-        """The reference's seed() is a no-op (:371-374); streams are fixed at construction."""
-        return [None if seed is None else seed + i for i in range(self.num_envs)]
+        """SB3 VecEnv.seed: env i draws the streams of seed + i from the next reset on (reference RNG: what
+        np.random.seed(seed + i); random.seed(seed + i) gives the reference; device RNG: the hash streams of
+        that seed from its first day).  seed=None picks a fresh seed.  The reference's own seed() is a no-op
+        (smart_nanogrid_environment.py:362-365) and it seeds through the global RNGs instead."""
+        if seed is None:
+            seed = int(np.random.SeedSequence().entropy % (2 ** 31))
+        seed = int(seed)
+        with torch.cuda.device(self.device):
+            check(lib().sng_set_seed(self._h, seed, _stream_handle(self.device)), self._h)
+        self._seed = seed
+        return [seed + i for i in range(self.num_envs)]
 
     def render(self, mode="human"):
         return None
 
+    # Per-env attributes get_attr / set_attr resolve env by env (the rest are shared by the batch: the
+    # reference's constructor keywords, settings, spaces, the timestep).
+    _PER_ENV_GET = {"random_pv_shift_ratio": "pv_ratio", "battery_state_of_charge": "battery_state_of_charge",
+                    "vehicle_state_of_charge": "vehicle_state_of_charge"}
+    _PER_ENV_SET = {"battery_state_of_charge": ("battery_state_of_charge", "set_battery_state_of_charge"),
+                    "vehicle_state_of_charge": ("vehicle_state_of_charge", "set_vehicle_state_of_charge")}
+
     def get_attr(self, attr_name, indices=None):
-        return [getattr(self.settings, attr_name, getattr(self, attr_name, None)) for _ in self._idx(indices)]
+        """SB3 VecEnv.get_attr: the attribute's value for each env of `indices` (AttributeError if unknown)."""
+        idx = self._idx(indices)
+        if attr_name in self._PER_ENV_GET:
+            values = getattr(self, self._PER_ENV_GET[attr_name])()
+            return [values[i] for i in idx]
+        if attr_name in ("timestep",):
+            return [self.timestep for _ in idx]
+        for owner in (self.settings, self):
+            if hasattr(owner, attr_name):
+                v = getattr(owner, attr_name)
+                return [v for _ in idx]
+        raise AttributeError(f"SmartNanogridVecEnv has no attribute {attr_name!r}")
 
     def set_attr(self, attr_name, value, indices=None):
-        setattr(self.settings, attr_name, value)
+        """SB3 VecEnv.set_attr.  Per-env state (battery / vehicle state of charge) is set for the given envs
+        only; a batch-wide setting (the constructor keywords, settings) can only be set for every env."""
+        idx = self._idx(indices)
+        if attr_name in self._PER_ENV_SET:
+            getter, setter = self._PER_ENV_SET[attr_name]
+            cur = getattr(self, getter)()
+            cur[idx] = value
+            getattr(self, setter)(cur)
+            return
+        if sorted(set(idx)) != list(range(self.num_envs)):
+            raise ValueError(f"{attr_name!r} is shared by every env of the batch: set it with indices=None")
+        if hasattr(self.settings, attr_name):
+            setattr(self.settings, attr_name, value)
+        elif hasattr(self, attr_name):
+            setattr(self, attr_name, value)
+        else:
+            raise AttributeError(f"SmartNanogridVecEnv has no attribute {attr_name!r}")
 
-    def env_method(self, method_name, *args, indices=None, **kwargs):
-        return [getattr(self, method_name)(*args, **kwargs) for _ in self._idx(indices)][:1] * len(self._idx(indices))
+    def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+        """SB3 VecEnv.env_method: one result per env of `indices`.  get_scenario is called per env; a
+        method that returns per-env values (an array with num_envs rows) is sliced per env; any other
+        method acts on the whole batch and needs indices=None."""
+        idx = self._idx(indices)
+        if method_name == "get_scenario":
+            return [self.get_scenario(i, *method_args, **method_kwargs) for i in idx]
+        fn = getattr(self, method_name)
+        if method_name not in self._PER_ENV_QUERIES and sorted(set(idx)) != list(range(self.num_envs)):
+            raise ValueError(f"{method_name!r} acts on the whole batch: call it with indices=None")
+        out = fn(*method_args, **method_kwargs)
+        if isinstance(out, (np.ndarray, list, tuple)) and len(out) == self.num_envs:
+            return [out[i] for i in idx]
+        return [out for _ in idx]
+
+    _PER_ENV_QUERIES = {"battery_state_of_charge", "pv_ratio", "vehicle_state_of_charge", "last_info_rows"}
 
     def env_is_wrapped(self, wrapper_class, indices=None):
         return [False for _ in self._idx(indices)]
@@ -304,10 +393,13 @@ class SmartNanogridVecEnv:
 
     def _idx(self, indices):
         if indices is None:
-            return range(self.num_envs)
-        if isinstance(indices, int):
-            return [indices]
-        return indices
+            return list(range(self.num_envs))
+        if isinstance(indices, (int, np.integer)):
+            indices = [int(indices)]
+        idx = [int(i) for i in indices]
+        if any(i < 0 or i >= self.num_envs for i in idx):
+            raise IndexError("env index out of range")
+        return idx
 
     # ------------------------------------------------------------------ helpers
     def _obs_to_host(self):
@@ -338,46 +430,94 @@ class SmartNanogridVecEnv:
         out["episode_return"] = self.return_d.cpu().numpy()
         return out
 
-    def battery_state_of_charge(self):
-        out = np.zeros(self.num_envs)
-        check(lib().sng_get_battery_soc(self._h, out.ctypes.data_as(_native.c_double_p)), self._h)
+    def last_info_rows(self):
+        """last_info() as one dict per env."""
+        info = self.last_info()
+        return [{k: v[i] for k, v in info.items()} for i in range(self.num_envs)]
+
+    def _host_array(self, fn, shape, value=None):
+        out = np.zeros(shape) if value is None else np.ascontiguousarray(np.broadcast_to(
+            np.asarray(value, np.float64), shape))
+        with torch.cuda.device(self.device):
+            check(fn(self._h, out.ctypes.data_as(_native.c_double_p), _stream_handle(self.device)), self._h)
         return out
+
+    def battery_state_of_charge(self):
+        return self._host_array(lib().sng_get_battery_soc, (self.num_envs,))
 
     def set_battery_state_of_charge(self, soc):
-        v = np.ascontiguousarray(np.broadcast_to(np.asarray(soc, np.float64), (self.num_envs,)))
-        check(lib().sng_set_battery_soc(self._h, v.ctypes.data_as(_native.c_double_p)), self._h)
+        self._host_array(lib().sng_set_battery_soc, (self.num_envs,), soc)
 
     def pv_ratio(self):
-        out = np.zeros(self.num_envs)
-        check(lib().sng_get_pv_ratio(self._h, out.ctypes.data_as(_native.c_double_p)), self._h)
-        return out
+        return self._host_array(lib().sng_get_pv_ratio, (self.num_envs,))
 
     def vehicle_state_of_charge(self):
-        out = np.zeros((self.num_envs, self.settings.number_of_chargers))
-        check(lib().sng_get_vehicle_soc(self._h, out.ctypes.data_as(_native.c_double_p)), self._h)
-        return out
+        return self._host_array(lib().sng_get_vehicle_soc, (self.num_envs, self.settings.number_of_chargers))
 
-    def get_scenario(self, env_index=0, max_vehicles=32):
-        """The current day of env `env_index` as the reference's initial_values.json dict
-        (ChargingStation.generated_initial_values_json, charging_station.py:164-191) and its PV
-        ratio, decoded from the device timeline (sng_get_scenario in include/sng.h)."""
+    def set_vehicle_state_of_charge(self, soc):
+        self._host_array(lib().sng_set_vehicle_soc, (self.num_envs, self.settings.number_of_chargers), soc)
+
+    def day_counter(self):
+        """Device-RNG days started so far (the day the next device reset draws)."""
+        out = ctypes.c_uint64()
+        with torch.cuda.device(self.device):
+            check(lib().sng_get_day_counter(self._h, ctypes.byref(out), _stream_handle(self.device)), self._h)
+        return out.value
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def save_state(self):
+        """The whole simulation state (sng_get_state: EV and BESS SoC, the loaded day, timestep, day counter,
+        RNG streams, the running day returns) as bytes, for load_state on a handle of the same configuration."""
+        size = ctypes.c_size_t()
+        check(lib().sng_state_size(self._h, 1, ctypes.byref(size)), self._h)
+        buf = np.empty(size.value, np.uint8)
+        with torch.cuda.device(self.device):
+            check(lib().sng_get_state(self._h, buf.ctypes.data_as(ctypes.c_void_p), size.value,
+                                      ctypes.c_void_p(self.return_d.data_ptr()), _stream_handle(self.device)),
+                  self._h)
+        return buf.tobytes()
+
+    def load_state(self, blob):
+        """Restore a save_state() blob (the day continues from its timestep)."""
+        buf = np.frombuffer(blob, np.uint8)
+        with torch.cuda.device(self.device):
+            check(lib().sng_set_state(self._h, buf.ctypes.data_as(ctypes.c_void_p), buf.size,
+                                      ctypes.c_void_p(self.return_d.data_ptr()), _stream_handle(self.device)),
+                  self._h)
+        self._seed = None
+
+    # ------------------------------------------------------------------ the loaded day
+    def get_scenarios(self, first=0, count=None, max_vehicles=8):
+        """The current days of envs [first, first + count) as the reference's initial_values.json dicts
+        (ChargingStation.generated_initial_values_json, charging_station.py:164-191) and their PV ratios,
+        decoded from the device timeline (sng_get_scenario in include/sng.h)."""
+        count = self.num_envs - first if count is None else int(count)
         N, S, V = self.settings.number_of_chargers, self.slots, int(max_vehicles)
-        f = [np.zeros((N, S)) for _ in range(4)]
-        arr = np.full((N, V), -1, np.int32)
-        dep = np.full((N, V), -1, np.int32)
-        nv = np.zeros(N, np.int32)
-        ratio = ctypes.c_double()
+        f = [np.zeros((count, N, S)) for _ in range(4)]
+        arr = np.full((count, N, V), -1, np.int32)
+        dep = np.full((count, N, V), -1, np.int32)
+        nv = np.zeros((count, N), np.int32)
+        ratio = np.zeros(count)
         P, I = _native.c_double_p, _native.c_int32_p
-        check(lib().sng_get_scenario(self._h, int(env_index), V, *[a.ctypes.data_as(P) for a in f],
-                                     arr.ctypes.data_as(I), dep.ctypes.data_as(I), nv.ctypes.data_as(I),
-                                     ctypes.byref(ratio)), self._h)
+        with torch.cuda.device(self.device):
+            check(lib().sng_get_scenario(self._h, int(first), count, V, *[a.ctypes.data_as(P) for a in f],
+                                         arr.ctypes.data_as(I), dep.ctypes.data_as(I), nv.ctypes.data_as(I),
+                                         ratio.ctypes.data_as(P), _stream_handle(self.device)), self._h)
         if (nv > V).any():
-            return self.get_scenario(env_index, int(nv.max()))
+            return self.get_scenarios(first, count, int(nv.max()))
         soc, occ, cap, req = f
-        iv = {"SOC": soc.tolist(), "Arrivals": [arr[c, :nv[c]].tolist() for c in range(N)],
-              "Departures": [dep[c, :nv[c]].tolist() for c in range(N)], "Charger_occupancy": occ.tolist(),
-              "Vehicle_capacities": cap.tolist(), "Requested_SOC": req.tolist()}
-        return iv, ratio.value
+        out = []
+        for k in range(count):
+            out.append({"SOC": soc[k].tolist(), "Arrivals": [arr[k, c, :nv[k, c]].tolist() for c in range(N)],
+                        "Departures": [dep[k, c, :nv[k, c]].tolist() for c in range(N)],
+                        "Charger_occupancy": occ[k].tolist(), "Vehicle_capacities": cap[k].tolist(),
+                        "Requested_SOC": req[k].tolist()})
+        return out, ratio
+
+    def get_scenario(self, env_index=0, max_vehicles=8):
+        """The current day of env `env_index` (get_scenarios for one env): (initial_values dict, PV ratio)."""
+        ivs, ratio = self.get_scenarios(int(env_index), 1, max_vehicles)
+        return ivs[0], float(ratio[0])
 
     def time_step_kernels(self, actions, days=1):
         """Device time (ms) of every step kernel over `days` eager device-RNG days, from HIP

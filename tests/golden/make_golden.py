@@ -18,12 +18,13 @@ Harness (the reference cannot be imported as shipped here, see SURVEY.md section
      by a hook that records the event and continues (what "continue" in pdb does).
 
 Seeding follows the reference's own contract: global `np.random.seed(s)` and
-`random.seed(s)` before `reset()` (`smart_nanogrid_environment.py:358`,
+`random.seed(s)` before `reset()` (`smart_nanogrid_environment.py:349`,
 `charging_station.py:214-279`).  Actions come from an independent
 `np.random.default_rng(seed ^ 0x5eed)` stream, float32, uniform in the action Box,
 about 20 % forced to exactly 0 and 5 % forced to exactly the upper bound.
 
-Usage:  python tests/golden/make_golden.py     (rewrites tests/golden/*.npz, *.json)
+Usage:  python tests/golden/make_golden.py        (rewrites tests/golden/*.npz, *.json)
+        python tests/golden/make_golden.py eval   (only the evaluator replay cases, eval_*.npz)
 """
 import builtins
 import json
@@ -201,6 +202,73 @@ def run_case(Env, name, kwargs, seed, n_episodes, act_override=None, persist_bet
     return out, meta
 
 
+def run_evaluator_case(Env, name, kwargs, seed, n_models, n_episodes, act_override=None):
+    """The loop of solvers/evaluator.py:88-101 on one env (the evaluator shares one env per variant):
+    per episode, model 0's reset generates the day (generate_new_initial_values=True, which writes
+    initial_values.json, charging_station.py:185-186) and every further model replays it
+    (generate_new_initial_values=False -> load_initial_values, :119-136: Requested_SOC is not restored,
+    the PV ratio is redrawn, smart_nanogrid_environment.py:349).  Model m's actions come from its own
+    stream default_rng((seed ^ 0x5EED) + 101 * m), one day of actions per episode."""
+    np.random.seed(seed)
+    random.seed(seed)
+    env = Env(**kwargs)
+    cms = env.central_management_system
+    T = int(24 / env.TIME_INTERVAL)
+    N = env.NUMBER_OF_CHARGERS
+    act_rngs = [np.random.default_rng((seed ^ 0x5EED) + 101 * m) for m in range(n_models)]
+    captured = {}
+    orig = cms.simulate
+
+    def spy(timestep, actions, ratio):
+        res = orig(timestep, actions, ratio)
+        captured["res"] = res
+        return res
+
+    cms.simulate = spy
+    rec = {k: [] for k in ["obs_reset", "obs", "reward", "done", "actions", "ratio", "bess_soc_reset", "generated",
+                           "soc0", "occ", "cap", "req", "arrivals", "departures"] + list(RESULT_KEYS)}
+    for ep in range(n_episodes):
+        for m in range(n_models):
+            generate = m == 0
+            bess_before = cms.battery_system.current_state_of_charge if cms.battery_system else 0.0
+            obs0, _ = env.reset(generate_new_initial_values=generate, algorithm_used="PPO",
+                                environment_mode="evaluation")
+            gv = cms.charging_station.generated_initial_values
+            rec["obs_reset"].append(np.asarray(obs0, np.float32))
+            rec["ratio"].append(env.random_pv_shift_ratio)
+            rec["bess_soc_reset"].append(bess_before)
+            rec["generated"].append(generate)
+            rec["soc0"].append(np.array(gv["SOC"], np.float64))
+            rec["occ"].append(np.array(gv["Charger_occupancy"], np.float64))
+            rec["cap"].append(np.array(gv["Vehicle_capacities"], np.float64))
+            rec["req"].append(np.array(gv["Requested_SOC"], np.float64))
+            arr = np.full((N, VMAX), -1, np.int64)
+            dep = np.full((N, VMAX), -1, np.int64)
+            for c in range(N):
+                arr[c, :len(gv["Arrivals"][c])] = gv["Arrivals"][c]
+                dep[c, :len(gv["Departures"][c])] = gv["Departures"][c]
+            rec["arrivals"].append(arr)
+            rec["departures"].append(dep)
+            rng = act_rngs[m]
+            acts = make_actions(rng, env.action_space, T) if act_override is None else act_override(rng, env, T)
+            rec["actions"].append(acts)
+            rows = {k: [] for k in ["obs", "reward", "done"] + list(RESULT_KEYS)}
+            for t in range(T):
+                obs, reward, term, trunc, info = env.step(acts[t].copy())
+                r = captured["res"]
+                rows["obs"].append(np.asarray(obs, np.float32))
+                rows["reward"].append(float(reward))
+                rows["done"].append(bool(term))
+                for k, rk in RESULT_KEYS.items():
+                    rows[k].append(float(r[rk]))
+            for k, v in rows.items():
+                rec[k].append(np.array(v))
+    out = {k: np.array(v) for k, v in rec.items()}
+    meta = dict(name=name, kwargs=kwargs, seed=seed, n_models=n_models, n_episodes=n_episodes, T=T, N=N,
+                obs_dim=int(env.observation_space.shape[0]), act_dim=int(env.action_space.shape[0]))
+    return out, meta
+
+
 def base_kwargs(**over):
     kw = dict(price_model=0, number_of_chargers=10, pv_system_available_in_model=True,
               battery_system_available_in_model=True, vehicle_to_everything=False,
@@ -255,6 +323,16 @@ CASES = [
 ]
 
 
+# solvers/evaluator.py:88-101 replays (reset True, then False for the other models), per episode
+EVAL_CASES = [
+    # name, kwargs, seed, models, episodes, action override
+    ("eval_replay_req_dense_n10", base_kwargs(enable_requested_state_of_charge=True,
+                                              vehicle_uncharged_penalty_mode="dense"), 91, 3, 2, None),
+    ("eval_replay_sparse_n4", base_kwargs(number_of_chargers=4), 92, 3, 2, None),
+    ("eval_replay_dod_n10", base_kwargs(), 93, 3, 2, heavy_discharge),
+]
+
+
 def tables_fixture(Env, tmp):
     """Derived per-dt constant tables straight from the reference objects."""
     out = {}
@@ -279,10 +357,29 @@ def tables_fixture(Env, tmp):
     return out
 
 
+def main_eval(Env):
+    index = []
+    for name, kw, seed, models, eps, override in EVAL_CASES:
+        out, meta = run_evaluator_case(Env, name, kw, seed, models, eps, override)
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **out)
+        index.append(meta)
+        print(f"{name}: N={meta['N']} models={models} episodes={eps} "
+              f"returns={[round(float(r.sum()), 4) for r in out['reward']]}")
+    with open(os.path.join(HERE, "eval_cases.json"), "w") as fp:
+        json.dump(index, fp, indent=1)
+
+
 def main():
     tmp = tempfile.mkdtemp(prefix="sng_golden_")
+    if sys.argv[1:] == ["eval"]:   # only the evaluator replay cases
+        try:
+            main_eval(import_reference(tmp))
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     try:
         Env = import_reference(tmp)
+        main_eval(Env)
         index = []
         for name, kw, seed, eps, override in CASES:
             out, meta = run_case(Env, name, kw, seed, eps, override)

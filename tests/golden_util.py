@@ -18,6 +18,17 @@ def case(name):
     return meta, np.load(os.path.join(GOLDEN, f"{name}.npz"))
 
 
+def eval_cases():
+    """The solvers/evaluator.py:88-101 replay cases (make_golden.py run_evaluator_case)."""
+    with open(os.path.join(GOLDEN, "eval_cases.json")) as fp:
+        return json.load(fp)
+
+
+def eval_case(name):
+    meta = [m for m in eval_cases() if m["name"] == name][0]
+    return meta, np.load(os.path.join(GOLDEN, f"{name}.npz"))
+
+
 def load_case(meta):
     return np.load(os.path.join(GOLDEN, f"{meta['name']}.npz"))
 

@@ -124,3 +124,32 @@ def test_gloo_world2_overlapped_day_return_exchange():
     for rep, got in enumerate(results):
         want = np.concatenate([base + 1000 * r + 100 * rep for r in range(2)], axis=1)
         np.testing.assert_array_equal(got, want)
+
+
+def _unequal_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    off, cnt = shard_envs(5, world, rank)   # 3 and 2 envs: the single-buffer gather cannot take them
+    try:
+        all_gather_returns(torch.zeros(cnt, dtype=torch.float64))
+        q.put((rank, "gathered"))
+    except ValueError as e:
+        q.put((rank, "ValueError" if "differ in size" in str(e) else str(e)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_unequal_shards_raise_on_every_rank():
+    """unequal shards must fail on every rank together, before any mismatched collective."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_unequal_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = sorted(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == [(0, "ValueError"), (1, "ValueError")]

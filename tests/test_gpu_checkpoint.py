@@ -1,0 +1,82 @@
+"""GPU: checkpoint / resume through the C ABI (sng_get_state / sng_set_state).
+
+A day is stopped at t = 11, its state saved, and restored into a fresh handle created with another
+seed; the restored handle finishes the day and runs the next one bit for bit like the uninterrupted
+run (observations, rewards, dones, day returns, BESS and EV state of charge) -- for reference-RNG days
+(the MT19937 streams travel in the blob, so the next day's draws match) and device-RNG days (the day
+counter travels).  The state being carried is the reference's: EV SoC arrays (charger.py:16-19), the
+BESS SoC and the day's initial SoC (central_management_system.py:93-94), the timestep
+(smart_nanogrid_environment.py:312) and the loaded day.
+"""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from smart_nanogrid_gym import SmartNanogridVecEnv  # noqa: E402
+from smart_nanogrid_gym._native import NativeError  # noqa: E402
+
+
+def run(v, acts, t0, days):
+    out = []
+    for d in range(days):
+        if not (d == 0 and t0 > 0):
+            v.reset_tensors()
+        for t in range(t0 if d == 0 else 0, 24):
+            o, r, dn = v.step_tensors(acts[d, t])
+            out.append((o.clone(), r.clone(), dn.clone()))
+        out.append((v.return_d.clone(),))
+    return out
+
+
+@pytest.mark.parametrize("rng,mode,req", [("reference", "sparse", False), ("reference", "dense", True),
+                                          ("device", "sparse", False), ("device", "dense", True)])
+def test_resume_mid_day_bit_exact(rng, mode, req):
+    E, N = 1024, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode=mode, enable_requested_state_of_charge=req)
+    g = torch.Generator(device="cuda:0").manual_seed(7)
+    acts = torch.rand((2, 24, E, N + 1), generator=g, device="cuda:0")
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    a = SmartNanogridVecEnv(E, seed=11, rng=rng, **kw)
+    a.reset_tensors()
+    for t in range(11):
+        a.step_tensors(acts[0, t])
+    blob = a.save_state()
+    want = run(a, acts, 11, 2)
+    want_state = (a.battery_state_of_charge(), a.vehicle_state_of_charge())
+    b = SmartNanogridVecEnv(E, seed=999, rng=rng, **kw)   # another seed: the blob carries the streams
+    b.load_state(blob)
+    assert b.timestep == 11
+    got = run(b, acts, 11, 2)
+    assert len(got) == len(want)
+    for x, y in zip(got, want):
+        for p, q in zip(x, y):
+            assert torch.equal(p, q)
+    np.testing.assert_array_equal(b.battery_state_of_charge(), want_state[0])
+    np.testing.assert_array_equal(b.vehicle_state_of_charge(), want_state[1])
+    # the replayable day travels too
+    assert torch.equal(a.replay_tensors(), b.replay_tensors())
+    a.close()
+    b.close()
+
+
+def test_state_refuses_other_configuration():
+    E = 256
+    kw = dict(number_of_chargers=10, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+    a = SmartNanogridVecEnv(E, seed=1, **kw)
+    a.reset_tensors()
+    blob = a.save_state()
+    for other in [dict(kw, vehicle_uncharged_penalty_mode="dense"), dict(kw, number_of_chargers=9)]:
+        b = SmartNanogridVecEnv(E, seed=1, **other)
+        with pytest.raises(NativeError, match="configuration"):
+            b.load_state(blob)
+        b.close()
+    c = SmartNanogridVecEnv(E + 1, seed=1, **kw)
+    with pytest.raises(NativeError):
+        c.load_state(blob)
+    with pytest.raises(NativeError):
+        a.load_state(blob[:100])
+    c.close()
+    a.close()

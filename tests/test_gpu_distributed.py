@@ -1,0 +1,85 @@
+"""GPU + gloo: the multi-rank path with the real library.  Two ranks (processes) share the one GPU of
+the box, each holding its shard of one env population (env_offset from parallel.shard_envs), replay two
+device-RNG days as the bench does (EpisodeGraph with per-day return rows) and all-gather the day
+returns over gloo.  The gathered returns must equal one handle simulating the whole population: the
+sharding is exact, so the RCCL run of the 8-GPU bench gathers the same numbers."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+KW = dict(number_of_chargers=10, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+E_RANK, SEED, DAYS, WORLD = 4096, 31, 2, 2
+
+
+def _actions(total, device):
+    g = torch.Generator(device=device).manual_seed(5)
+    a = torch.rand((24, total, 11), generator=g, device=device)
+    a[..., -1] = a[..., -1] * 2 - 1
+    return a
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv
+        from smart_nanogrid_gym.parallel import all_gather_returns, shard_envs
+        off, cnt = shard_envs(world * E_RANK, world, rank)
+        dev = torch.device("cuda", 0)
+        acts = _actions(world * E_RANK, dev)[:, off:off + cnt].contiguous()
+        venv = SmartNanogridVecEnv(cnt, seed=SEED, rng="device", env_offset=off, **KW)
+        rows = torch.zeros((DAYS, cnt), dtype=torch.float64, device=dev)
+        g = EpisodeGraph(venv, acts, days=DAYS, day_returns=rows)
+        g.launch()
+        torch.cuda.synchronize()
+        gathered = [all_gather_returns(rows[d].cpu()) for d in range(DAYS)]   # gloo: host tensors
+        g.close()
+        venv.close()
+        if rank == 0:
+            q.put(np.stack([x.numpy() for x in gathered]))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_two_ranks_one_gpu_gather_equals_one_population():
+    import torch.multiprocessing as mp
+    from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    total = WORLD * E_RANK
+    dev = torch.device("cuda", 0)
+    full = SmartNanogridVecEnv(total, seed=SEED, rng="device", **KW)
+    rows = torch.zeros((DAYS, total), dtype=torch.float64, device=dev)
+    g = EpisodeGraph(full, _actions(total, dev), days=DAYS, day_returns=rows)
+    g.launch()
+    torch.cuda.synchronize()
+    want = rows.cpu().numpy()
+    g.close()
+    full.close()
+    assert gathered.shape == (DAYS, total)
+    np.testing.assert_array_equal(gathered, want)
+    assert np.isfinite(want).all() and (want < 0).mean() > 0.99

@@ -162,7 +162,8 @@ def test_device_day_decode_round_trip(N, req, dt):
     rng = np.random.default_rng(3)
     for t in range(a_dev.timesteps):
         a = torch.from_numpy(rng.uniform(-1, 1, (E, a_dev.act_dim)).astype(np.float32)).to(a_dev.device)
-        a = torch.where(a < 0, torch.zeros_like(a), a)
+        # chargers in their Box [0, 1]; the BESS action keeps its negative half (discharge, over-discharge clamp)
+        a[:, :N] = torch.where(a[:, :N] < 0, torch.zeros_like(a[:, :N]), a[:, :N])
         oa, ra, _ = a_dev.step_tensors(a)
         ob, rb, _ = b_inj.step_tensors(a)
         assert torch.equal(oa, ob), t

@@ -1,0 +1,176 @@
+"""GPU: the SB3 VecEnv contract and the C ABI's state getters.
+
+* seed() reseeds: after venv.seed(s) the next days are those of a fresh population seeded s (both RNG
+  modes; SB3 VecEnv.seed semantics, env i <- s + i).
+* get_attr / set_attr / env_method honour `indices` env by env, and raise for unknown names or for
+  batch-wide settings set on a subset.
+* ABI getters report argument errors through sng_last_error and synchronise only the caller's stream.
+* Device-RNG days of wide stations (N > 16: the generator without its fused t = 0 blocks) draw their PV
+  ratio and zero the t = 0 penalty like the fused path, and every device day advances the day counter
+  exactly once.
+* A steps-only graph refuses a day of another encoding and a start after t = 0.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv  # noqa: E402
+from smart_nanogrid_gym import _native  # noqa: E402
+from smart_nanogrid_gym._native import NativeError, lib  # noqa: E402
+
+KW = dict(number_of_chargers=10, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+
+
+@pytest.mark.parametrize("rng", ["reference", "device"])
+def test_seed_reseeds_the_streams(rng):
+    E = 512
+    a = SmartNanogridVecEnv(E, seed=1, rng=rng, **KW)
+    a.reset_tensors()
+    for t in range(24):
+        a.step_tensors(torch.zeros((E, 11), device="cuda:0"))
+    assert a.seed(77) == [77 + i for i in range(E)]
+    b = SmartNanogridVecEnv(E, seed=77, rng=rng, **KW)
+    for day in range(2):
+        oa, ob = a.reset_tensors().clone(), b.reset_tensors().clone()
+        assert torch.equal(oa[:, :-1], ob[:, :-1]), day     # the BESS entry carries a's history
+        assert a.get_scenarios()[0] == b.get_scenarios()[0]
+        np.testing.assert_array_equal(a.pv_ratio(), b.pv_ratio())
+        for t in range(24):
+            a.step_tensors(torch.zeros((E, 11), device="cuda:0"))
+            b.step_tensors(torch.zeros((E, 11), device="cuda:0"))
+    a.close()
+    b.close()
+
+
+def test_attributes_and_methods_per_index():
+    E = 8
+    v = SmartNanogridVecEnv(E, seed=4, **KW)
+    v.reset()
+    ratio = v.pv_ratio()
+    assert v.get_attr("random_pv_shift_ratio", [1, 5]) == [ratio[1], ratio[5]]
+    assert v.get_attr("number_of_chargers") == [10] * E
+    assert v.get_attr("timestep", 3) == [0]
+    with pytest.raises(AttributeError):
+        v.get_attr("no_such_attribute")
+    v.set_attr("battery_state_of_charge", 0.25, [1, 3])
+    soc = v.battery_state_of_charge()
+    assert soc[1] == soc[3] == 0.25 and soc[0] == soc[2] == 0.5
+    with pytest.raises(ValueError):
+        v.set_attr("algorithm_used", "PPO", [0])
+    v.set_attr("algorithm_used", "PPO")
+    assert v.get_attr("algorithm_used", [2]) == ["PPO"]
+    res = v.env_method("get_scenario", indices=[2, 6])
+    assert len(res) == 2 and res[0][1] == ratio[2] and res[1][1] == ratio[6]
+    assert v.env_method("battery_state_of_charge", indices=[3]) == [0.25]
+    with pytest.raises(ValueError):
+        v.env_method("reset_tensors", indices=[0])
+    assert len(v.env_method("pv_ratio")) == E
+    with pytest.raises(IndexError):
+        v.get_attr("random_pv_shift_ratio", [E])
+    v.close()
+
+
+def test_getters_report_errors_and_sync_the_callers_stream():
+    E = 4096
+    v = SmartNanogridVecEnv(E, seed=2, rng="device", **KW)
+    s = torch.cuda.Stream()
+    rc = lib().sng_get_battery_soc(v._h, None, ctypes.c_void_p(s.cuda_stream))
+    assert rc == -1 and b"null host array" in lib().sng_last_error(v._h)
+    rc = lib().sng_get_pv_ratio(v._h, None, None)
+    assert rc == -1 and b"sng_get_pv_ratio" in lib().sng_last_error(v._h)
+    # work queued on a side stream is seen by a getter ordered on that stream
+    with torch.cuda.stream(s):
+        _native.check(lib().sng_reset(v._h, _native.RNG_DEVICE, ctypes.c_void_p(v.obs_d.data_ptr()),
+                                      ctypes.c_void_p(s.cuda_stream)), v._h)
+        out = np.zeros(E)
+        _native.check(lib().sng_get_pv_ratio(v._h, out.ctypes.data_as(_native.c_double_p),
+                                             ctypes.c_void_p(s.cuda_stream)), v._h)
+    assert set(np.unique(np.round(out * 100))).issubset(set(range(181))) and out.std() > 0
+    v.close()
+
+
+@pytest.mark.parametrize("N", [10, 33, 50, 128])
+def test_device_days_draw_ratio_and_count_days_at_every_width(N):
+    """wide stations took a generator path that left the PV ratio at 1.0 and the day counter
+    advanced twice.  Every width must draw U{0..180}/100 ratios and advance the counter once a day."""
+    E = 8192 if N <= 50 else 2048
+    kw = dict(KW, number_of_chargers=N)
+    v = SmartNanogridVecEnv(E, seed=9, rng="device", **kw)
+    ratios = []
+    for day in range(3):
+        assert v.day_counter() == day
+        v.reset_tensors()
+        r = v.pv_ratio()
+        ratios.append(r)
+        assert set(np.unique(np.round(r * 100))).issubset(set(range(181)))
+        assert abs(r.mean() - 0.9) < 0.05 and r.std() > 0.4
+        for t in range(24):
+            v.step_tensors(torch.zeros((E, N + 1), device="cuda:0"))
+    assert v.day_counter() == 3
+    assert not np.array_equal(ratios[0], ratios[1])
+    v.close()
+
+
+@pytest.mark.parametrize("N", [10, 50])
+def test_device_reset_zeroes_the_injected_t0_penalty(N):
+    """A day injected with a penalised vehicle in the python index -1 slot has a t = 0 penalty; the next
+    device-RNG reset must start from 0 again (fused and separate t = 0 paths).  The twin runs the same
+    injected day without that slot, so both advance the day counter alike."""
+    E = 256
+    kw = dict(KW, number_of_chargers=N, vehicle_uncharged_penalty_mode="dense")
+    a = SmartNanogridVecEnv(E, seed=6, rng="device", **kw)
+    b = SmartNanogridVecEnv(E, seed=6, rng="device", **kw)
+    S = 25
+    soc, occ, cap, req = (np.zeros((E, N, S)) for _ in range(4))
+    occ[:, :, :5] = 1
+    cap[:, :, :5] = 40
+    soc[:, :, 0] = 0.5
+    arr = np.zeros((E, N, 1), np.int32)
+    dep = np.full((E, N, 1), 5, np.int32)
+    soc_a, req_a = soc.copy(), req.copy()
+    soc_a[:, :, 24] = 0.2
+    req_a[:, :, 24] = 1.0                                     # python index -1: SOC 0.2, requested 1.0
+    a.reset_from_arrays(soc_a, occ, cap, req_a, arr, dep, np.ones(E))
+    b.reset_from_arrays(soc, occ, cap, req, arr, dep, np.ones(E))
+    zero = torch.zeros((E, N + 1), device="cuda:0")
+    _, r0, _ = a.step_tensors(zero)
+    assert float(r0.max()) <= -64.0 * N + 1e-6                # the injected t = 0 penalty is there
+    _, r0b, _ = b.step_tensors(zero)
+    assert float(r0b.min()) > -64.0
+    for t in range(1, 24):
+        a.step_tensors(zero)
+        b.step_tensors(zero)
+    oa, ob = a.reset_tensors().clone(), b.reset_tensors().clone()
+    assert torch.equal(oa, ob)
+    _, ra, _ = a.step_tensors(zero)
+    ra = ra.clone()
+    _, rb, _ = b.step_tensors(zero)
+    assert torch.equal(ra, rb)
+    a.close()
+    b.close()
+
+
+def test_steps_only_graph_refuses_other_encodings():
+    E, N = 512, 10
+    kw = dict(KW, vehicle_uncharged_penalty_mode="dense")
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    v = SmartNanogridVecEnv(E, seed=8, rng="reference", **kw)
+    v.reset_tensors()
+    iv, r = v.get_scenarios()
+    for d in iv:   # a penalised requested SoC below 1: the injected day carries a requested-SoC stream
+        d["Requested_SOC"] = [[0.9 if x else 0.0 for x in row] for row in d["Charger_occupancy"]]
+    v.reset_from_initial_values(iv, r, restore_requested_soc=True)
+    g = EpisodeGraph(v, acts, with_reset=False)
+    v.reset_tensors()                   # reference RNG without requested SoC: no stream
+    with pytest.raises(NativeError, match="another encoding"):
+        g.launch()
+    v.reset_from_initial_values(iv, r, restore_requested_soc=True)
+    g.launch()                          # the same encoding again: allowed
+    with pytest.raises(NativeError, match="t = 0"):
+        g.launch()
+    g.close()
+    v.close()

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 import oracle as O
-from golden_util import case, cases, kat, load_case
+from golden_util import case, cases, eval_case, eval_cases, kat, load_case
 
 CASES = [m["name"] for m in cases()]
 SCALARS = ["grid_power", "p_charge", "p_discharge", "bess_soc", "pen_vehicle", "pen_battery", "grid_cost",
@@ -91,3 +91,32 @@ def test_oracle_numpy2_promotion_close_to_recording(sub):
         _, r, _, info = env.step(k["actions"][t])
         assert abs(info["grid_power"] - pr["Grid_power"][t]) < 2e-6
         assert abs(info["total_cost"] - pr["Total_cost"][t]) < 2e-6
+
+
+@pytest.mark.parametrize("name", [m["name"] for m in eval_cases()])
+def test_oracle_replays_like_the_reference_evaluator(name):
+    """solvers/evaluator.py:88-101 on the reference: reset(generate_new_initial_values=True) for the first
+    model of an episode, False for the others (load_initial_values: same vehicles, Requested_SOC not
+    restored, a new PV ratio).  The oracle's replay matches it bit for bit, per model and episode."""
+    meta, d = eval_case(name)
+    cfg = O.OracleConfig(**meta["kwargs"])
+    env = O.OracleEnv(cfg, meta["seed"])
+    k = 0
+    for ep in range(meta["n_episodes"]):
+        for m in range(meta["n_models"]):
+            assert bool(d["generated"][k]) == (m == 0)
+            obs = env.reset() if m == 0 else env.replay()
+            np.testing.assert_array_equal(obs, d["obs_reset"][k])
+            assert env.ratio == d["ratio"][k]
+            assert env.bess_soc == d["bess_soc_reset"][k]
+            for t in range(meta["T"]):
+                obs, r, done, info = env.step(d["actions"][k][t])
+                np.testing.assert_array_equal(obs, d["obs"][k][t])
+                assert r == d["reward"][k][t], (ep, m, t)
+                for key in SCALARS:
+                    assert info[key] == d[key][k][t], (key, ep, m, t)
+                if m > 0:   # a replayed day never penalises a vehicle (Requested_SOC = 0)
+                    assert info["pen_vehicle"] == 0.0
+            k += 1
+    # the generated days penalise (dense / sparse modes), so the replay's zero penalty is a real difference
+    assert d["pen_vehicle"][0].sum() > 0

@@ -61,7 +61,7 @@ def test_file_names_follow_the_reference(kw, stem):
 
 
 def test_recorded_soc_is_the_oracle_day_end_array():
-    """'SOC' in the recorded file is the charger arrays after the day (charger.py:36-53 rewrite
+    """'SOC' in the recorded file is the charger arrays after the day (charger.py:37-56 rewrite
     SOC[c, t] at every occupied step): the oracle's arrays after replaying the day."""
     k = kat("training_files")
     iv = k["iv"]
