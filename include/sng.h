@@ -304,6 +304,22 @@ int32_t sng_host_threads(void);
  * reset draws day *out).  Synchronises `stream`. */
 int sng_get_day_counter(SngEnv *env, uint64_t *out, void *stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Multi-GPU exchange: one process per GPU, each with its contiguous env shard
+ * (sng_set_env_offset); once per simulated day the per-env returns are all-gathered over RCCL
+ * (xGMI within a node).  No per-step communication.  RCCL is loaded at the first call
+ * (dlopen librccl.so.1).  Rank 0 makes the id with sng_comm_unique_id and hands it to every rank
+ * (file, socket, MPI ...); each rank then calls sng_comm_create with it. */
+#define SNG_COMM_ID_BYTES 128
+typedef struct SngComm SngComm;
+int sng_comm_unique_id(uint8_t *id /* [SNG_COMM_ID_BYTES] */);
+int sng_comm_create(int device, int nranks, int rank, const uint8_t *id, SngComm **out);
+/* local: device [count] f64 of this rank; global: device [nranks * count] f64, rank-major (= global
+ * env order for equal contiguous shards).  Asynchronous on `stream`. */
+int sng_allgather_returns(SngComm *comm, const double *local, double *global, int64_t count, void *stream);
+void sng_comm_destroy(SngComm *comm);
+const char *sng_comm_last_error(const SngComm *comm);   /* NULL: the calling thread's last create error */
+
 #ifdef __cplusplus
 }
 #endif

@@ -27,6 +27,13 @@
 namespace sng {
 
 constexpr int kWave = 64;
+// Live lanes (envs) per wavefront of the one-lane step kernel: 64, or 32 with SNG_V_HALF (A/B build:
+// two wavefronts per SIMD at E = 65,536, each with half its lanes idle).
+#ifdef SNG_V_HALF
+constexpr int kLive = 32;
+#else
+constexpr int kLive = 64;
+#endif
 
 // Streaming (nontemporal) stores for the step's bulk outputs (SoC, observations): they leave
 // less dirty L2 for the end-of-kernel release (measured 8.92 -> 8.17 us per step at 65,536 x 10).
@@ -355,6 +362,14 @@ __device__ __forceinline__ double div_by_cap(double x, double c, double r) {
 // SoC at python index t-1.  Charger.charge_or_discharge_vehicle (charger.py:37-56, 58-94,
 // 108-144) and reset_info_values (:146-156).
 // ---------------------------------------------------------------------------------
+// Penaliser.penalise_state_of_charge_outside_margin (penaliser.py:71-87), insufficient branch, for a
+// charger in the penalty-check list (W_PEN): SoC and requested SoC at python index t-1.
+__device__ __forceinline__ double pen_term(uint32_t w, double run, double req) {
+    const double margin = 0.05 * req;
+    const double d = (req - run) * 10;
+    return ((w & W_PEN) && (run < req - margin)) ? d * d : 0.0;
+}
+
 struct ChargerResult {
     double pw;      // charger power value (kW), f64 array element of charging_station.py:282
     double q;       // insufficient-charge penalty term (0 if not checked / not insufficient)
@@ -525,8 +540,8 @@ template <int NC, int L>
 struct StepLds {
     static constexpr int BLOCK = step_block(NC);
     static constexpr int WAVES = BLOCK / kWave;
-    static constexpr int WENVS = kWave / L;             // envs per wavefront
-    static constexpr int ENVS = BLOCK / L;               // envs per workgroup
+    static constexpr int WENVS = (L == 1 ? kLive : kWave) / L;   // envs per wavefront
+    static constexpr int ENVS = WAVES * WENVS;           // envs per workgroup
     static constexpr bool kRows = NC > 0 && NC <= 16;   // compacted power rows (else PairwiseSum)
     __host__ __device__ static int act_floats(int A) { return round4(WENVS * A); }
     __host__ __device__ static int obs_floats(int O) { return round4(WENVS * O); }
@@ -619,7 +634,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     // branch separates it from the per-charger loads, so the wait before the commits is
     // vmcnt(#per-charger loads) and charger c's update starts as soon as its own loads land.
     // Non-live lanes load a valid env (E - 1) and discard it.
-    const int64_t el = live ? e : E - 1;
+    const int64_t el = live ? e : (le < WENVS ? E - 1 : e0);   // idle lanes (SNG_V_HALF) read lane 0's lines
     const uint32_t lo = (uint32_t)(el - e0);   // lane offset from the wave's first env
     const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;   // byte offsets of the env
     const uint32_t *__restrict__ word_t = word + tbase * (size_t)E;   // this step's timeline planes
@@ -755,6 +770,23 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     double pen_v = 0.0;
     uint32_t n_nonexist = 0;
     uint32_t fl = 0;
+#if defined(SNG_V_NEGSKIP)
+    // Only a negative action makes a charger power negative (charger_step: moved && !chg), so a
+    // wavefront none of whose live envs has one skips the discharging total's accumulation: it is
+    // the empty sum, +0.0, as numpy's P[P < 0].sum() (charging_station.py:293).  Wave-uniform.
+    double pwv[kRows ? (NC > 0 ? NC : 1) : 1];
+    auto add_pos = [&](double pw) {
+        row_pos[n_pos] = pw;
+        seq_pos += __builtin_fmax(pw, 0.0);
+        n_pos += (pw > 0.0) ? 1 : 0;
+    };
+    bool neg_lane = false;
+    if (kRows && live) {
+#pragma unroll
+        for (int c = 0; c < (NC > 0 ? NC : 1); ++c) neg_lane |= a_row[c] < 0.0f;
+    }
+    const bool wave_neg = __builtin_amdgcn_ballot_w64(neg_lane) != 0;
+#endif
     if (live) {
         for (int c0 = cbeg; c0 < cend; c0 += CH) {
             if (c0 != cbeg) load_batch(c0);
@@ -786,8 +818,21 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                 n_nonexist += r.nx;
                 fl |= r.fl;
                 if (L == 1) {
+#if defined(SNG_V_REQCONST)
+                    if (!kRows) pen_v += r.q;   // kRows: the penalty terms are summed after the loop
+#else
                     pen_v += r.q;
+#endif
+#if defined(SNG_V_NEGSKIP)
+                    if (kRows) {
+                        pwv[j] = r.pw;   // the negative powers are compacted after the loop, if any
+                        add_pos(r.pw);
+                    } else {
+                        add_power(r.pw);
+                    }
+#else
                     add_power(r.pw);
+#endif
                 } else {
                     s_pw[le * NC + c] = r.pw;
                     s_q[le * NC + c] = r.q;
@@ -799,6 +844,30 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             }
         }
     }
+#if defined(SNG_V_NEGSKIP)
+    if (kRows && L == 1 && live && wave_neg) {
+#pragma unroll
+        for (int c = 0; c < (NC > 0 ? NC : 1); ++c) {
+            const double pw = pwv[c];
+            row_neg[n_neg] = pw;
+            seq_neg += __builtin_fmin(pw, 0.0);
+            n_neg += (pw < 0.0) ? 1 : 0;
+        }
+    }
+#endif
+#if defined(SNG_V_REQCONST)
+    // the penalty terms in charger order (Python's sum over the list, penaliser.py:55); without a
+    // requested-SoC stream Requested_SOC is the literal 1.0 (threshold 0.95), on a replayed day 0
+    if (kRows && L == 1 && live && t > 0 && !p.req_zero) {
+        if (!p.req_stream) {
+#pragma unroll
+            for (int c = 0; c < (NC > 0 ? NC : 1); ++c) pen_v += pen_term(w[c], run[c], 1.0);
+        } else {
+#pragma unroll
+            for (int c = 0; c < (NC > 0 ? NC : 1); ++c) pen_v += pen_term(w[c], run[c], req[c]);
+        }
+    }
+#endif
     if (L > 1) {
         // gather the env's lanes (same wavefront): counts and flag bits, then in-order
         // penalty / power sums by the leader from LDS

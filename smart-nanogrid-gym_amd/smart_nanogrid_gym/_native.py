@@ -26,6 +26,7 @@ FLAG_NEGATIVE_DEMAND = 0x1
 FLAG_CHARGING_MODE = 0x2
 FLAG_BESS_SOC_ABOVE_1 = 0x4
 FLAG_V2X_BREAKPOINT = 0x8
+COMM_ID_BYTES = 128
 
 c_double_p = ctypes.POINTER(ctypes.c_double)
 c_float_p = ctypes.POINTER(ctypes.c_float)
@@ -139,6 +140,12 @@ EXPORTS = {
                                                    c_int32_p, c_int32_p, ctypes.c_int32, c_double_p]),
     "sng_host_threads": (ctypes.c_int32, []),
     "sng_get_day_counter": (ctypes.c_int, [_H, ctypes.POINTER(ctypes.c_uint64), _S]),
+    "sng_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
+    "sng_comm_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                                       ctypes.POINTER(ctypes.c_void_p)]),
+    "sng_allgather_returns": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _S]),
+    "sng_comm_destroy": (None, [ctypes.c_void_p]),
+    "sng_comm_last_error": (ctypes.c_char_p, [ctypes.c_void_p]),
 }
 
 _lib = None

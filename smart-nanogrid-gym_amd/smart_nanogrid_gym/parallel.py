@@ -98,6 +98,47 @@ class DayReturnExchange:
         return self.out[k].permute(1, 0, 2).reshape(d, w * e)
 
 
+class NativeComm:
+    """The C ABI's own RCCL exchange (sng_comm_create / sng_allgather_returns in include/sng.h) -- the
+    multi-GPU path a non-Python host uses.  Here the unique id travels over an existing
+    torch.distributed group (rank 0 makes it); a C host would use a file, a socket or MPI."""
+
+    def __init__(self, device, group=None):
+        import ctypes
+        from ._native import COMM_ID_BYTES, lib
+        self._lib = lib()
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        buf = ctypes.create_string_buffer(COMM_ID_BYTES)
+        if rank == 0:
+            self._check(self._lib.sng_comm_unique_id(buf), None)
+        ids = [buf.raw if rank == 0 else None]
+        dist.broadcast_object_list(ids, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        h = ctypes.c_void_p()
+        self._check(self._lib.sng_comm_create(int(device), world, rank, ids[0], ctypes.byref(h)), None)
+        self._h, self.world, self.rank, self.device = h, world, rank, int(device)
+
+    def _check(self, rc, handle):
+        if rc != 0:
+            msg = self._lib.sng_comm_last_error(handle)
+            raise RuntimeError(f"sng comm error {rc}: {msg.decode() if msg else ''}")
+
+    def all_gather_returns(self, local, out=None):
+        """[count] f64 device tensor per rank -> [world * count], rank-major, on the current stream."""
+        import ctypes
+        local = local.contiguous()
+        if out is None:
+            out = torch.empty(self.world * local.numel(), dtype=torch.float64, device=local.device)
+        stream = ctypes.c_void_p(torch.cuda.current_stream(local.device).cuda_stream)
+        self._check(self._lib.sng_allgather_returns(self._h, ctypes.c_void_p(local.data_ptr()),
+                                                    ctypes.c_void_p(out.data_ptr()), local.numel(), stream), self._h)
+        return out
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.sng_comm_destroy(self._h)
+            self._h = None
+
+
 def max_over_ranks(value, device=None, group=None):
     """Max of a host float over ranks (bench timing: the slowest rank defines the wall time)."""
     if not dist.is_available() or not dist.is_initialized():

@@ -83,3 +83,28 @@ def test_two_ranks_one_gpu_gather_equals_one_population():
     assert gathered.shape == (DAYS, total)
     np.testing.assert_array_equal(gathered, want)
     assert np.isfinite(want).all() and (want < 0).mean() > 0.99
+
+
+def test_native_rccl_exchange_world1():
+    """The C ABI's own RCCL exchange (sng_comm_create / sng_allgather_returns), world 1 on this box: the
+    gathered buffer is the rank's day returns (the 8-GPU gather is the driver's run)."""
+    import torch.distributed as dist
+    from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv
+    from smart_nanogrid_gym.parallel import NativeComm
+    dev = torch.device("cuda", 0)
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            device_id=dev)
+    try:
+        comm = NativeComm(0)
+        venv = SmartNanogridVecEnv(E_RANK, seed=SEED, rng="device", **KW)
+        rows = torch.zeros((DAYS, E_RANK), dtype=torch.float64, device=dev)
+        g = EpisodeGraph(venv, _actions(E_RANK, dev), days=DAYS, day_returns=rows)
+        g.launch()
+        out = comm.all_gather_returns(rows.reshape(-1))
+        torch.cuda.synchronize()
+        assert torch.equal(out, rows.reshape(-1)) and bool((out < 0).any())
+        comm.close()
+        g.close()
+        venv.close()
+    finally:
+        dist.destroy_process_group()
