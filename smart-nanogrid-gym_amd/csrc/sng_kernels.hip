@@ -27,13 +27,6 @@
 namespace sng {
 
 constexpr int kWave = 64;
-// Live lanes (envs) per wavefront of the one-lane step kernel: 64, or 32 with SNG_V_HALF (A/B build:
-// two wavefronts per SIMD at E = 65,536, each with half its lanes idle).
-#ifdef SNG_V_HALF
-constexpr int kLive = 32;
-#else
-constexpr int kLive = 64;
-#endif
 
 // Streaming (nontemporal) stores for the step's bulk outputs (SoC, observations): they leave
 // less dirty L2 for the end-of-kernel release (measured 8.92 -> 8.17 us per step at 65,536 x 10).
@@ -362,14 +355,6 @@ __device__ __forceinline__ double div_by_cap(double x, double c, double r) {
 // SoC at python index t-1.  Charger.charge_or_discharge_vehicle (charger.py:37-56, 58-94,
 // 108-144) and reset_info_values (:146-156).
 // ---------------------------------------------------------------------------------
-// Penaliser.penalise_state_of_charge_outside_margin (penaliser.py:71-87), insufficient branch, for a
-// charger in the penalty-check list (W_PEN): SoC and requested SoC at python index t-1.
-__device__ __forceinline__ double pen_term(uint32_t w, double run, double req) {
-    const double margin = 0.05 * req;
-    const double d = (req - run) * 10;
-    return ((w & W_PEN) && (run < req - margin)) ? d * d : 0.0;
-}
-
 struct ChargerResult {
     double pw;      // charger power value (kW), f64 array element of charging_station.py:282
     double q;       // insufficient-charge penalty term (0 if not checked / not insufficient)
@@ -540,7 +525,7 @@ template <int NC, int L>
 struct StepLds {
     static constexpr int BLOCK = step_block(NC);
     static constexpr int WAVES = BLOCK / kWave;
-    static constexpr int WENVS = (L == 1 ? kLive : kWave) / L;   // envs per wavefront
+    static constexpr int WENVS = kWave / L;              // envs per wavefront
     static constexpr int ENVS = WAVES * WENVS;           // envs per workgroup
     static constexpr bool kRows = NC > 0 && NC <= 16;   // compacted power rows (else PairwiseSum)
     __host__ __device__ static int act_floats(int A) { return round4(WENVS * A); }
@@ -579,6 +564,173 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// 1/c for an integer capacity c in [1, 255]: v_rcp_f64 and one Newton step.  div_by_cap needs only a
+// relative error far below 2^-31 here (its quotient then errs by < 2^-62 relative before the last
+// rounding, which x/c's distance from a rounding midpoint, >= 2^-62, absorbs): v_rcp_f64's error
+// squared by the Newton step is ~2^-46.  c = 0 (empty charger) gives NaN, which charger_step selects away.
+__device__ __forceinline__ double recip_cap(double c) {
+    const double r0 = __builtin_amdgcn_rcp(c);
+    return __builtin_fma(r0, __builtin_fma(-c, r0, 1.0), r0);
+}
+
+// ---------------------------------------------------------------------------------
+// The lean step: the one-lane, no-diagnostics, NumPy-2 / power-of-two-dt step of a station of
+// N <= 16 chargers (every configuration the bench and a training loop run), one wavefront per 64
+// envs.  Against the general kernel below it keeps nothing in LDS but the actions and observation
+// tiles: the step constants sit in scalar registers, 1/cap comes from recip_cap instead of an LDS
+// table (no per-wave table staging, no LDS round trip per charger), and the charging / discharging
+// totals are the running sums the lane keeps anyway whenever those equal numpy's pairwise sum of the
+// compacted arrays (charging_station.py:289-293) exactly:
+//   - fewer than 8 terms: numpy sums them sequentially (loops_utils.h.src), and the skipped +0.0
+//     terms leave a sum unchanged;
+//   - positive powers are float32 values (the NEP 50 product pc, charger.py:92-94, when charging);
+//     when the smallest of them, pmin, satisfies sum <= pmin * 2^28, every partial sum is a multiple
+//     of pmin's float32 ulp below 2^53 such ulps, so every addition is exact in any order.
+// Only a lane with 8 or more negative powers, or 8 or more positive ones whose sum is not provably
+// exact, compacts its powers into its LDS rows and runs the pairwise sum (rare; wave-uniform skip).
+// ---------------------------------------------------------------------------------
+template <int NC, bool PK>
+__device__ __forceinline__ void step_lean(const Params &p, const DeviceState &s, const InfoPtrs &info,
+                                          const float *__restrict__ act, float *__restrict__ obs,
+                                          double *__restrict__ reward, uint8_t *__restrict__ done, int64_t E, int t,
+                                          int vec_io, float *s_act, float *s_obs, double *s_pos, double *s_neg,
+                                          int64_t e0, int nw, int lane) {
+    constexpr int A = NC + 1;   // with the BESS action; without a BESS the tile is one float narrower
+    constexpr int KT = ((NC + 1) * kWave + 4 * kWave - 1) / (4 * kWave);
+    const int Ad = p.act_dim, O = p.obs_dim;
+    const bool live = lane < nw;
+    const int64_t el = live ? e0 + lane : E - 1;   // idle lanes load a valid env and discard it
+    const uint32_t lo = (uint32_t)(el - e0);
+    const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;
+    const size_t plane = (size_t)t * NC * (size_t)E;   // this step's timeline planes
+    const uint32_t *__restrict__ word_t = s.word + plane;
+    const double *__restrict__ aux_t = s.aux + plane;
+    const double *__restrict__ req_t = s.req + plane;
+
+    // 1. per-env values (pointer selects rather than branches: a disabled stream re-reads ratio)
+    const double ratio = bld(s.ratio, el8);
+    const double bess_l = bld(p.bess ? s.bess : s.ratio, el8);
+    const double pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
+    const double ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
+    double req[NC];
+    if (p.req_stream && !p.req_zero) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) req[c] = bld(req_t, el8, (uint32_t)c * (uint32_t)E * 8u);
+    } else {   // no stream: 1.0 (charging_station.py:230-232); a replayed day: the cleared 0.0
+        const double rq = p.req_zero ? 0.0 : 1.0;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) req[c] = rq;
+    }
+    double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
+    if (p.noise) {
+        const size_t pl = (size_t)(p.T + 3) * E;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            fpv[j] = bld(s.prof + (size_t)(t + j) * E, el8);
+            fpr[j] = bld(s.prof + pl + (size_t)(t + j) * E, el8);
+        }
+    }
+    // 2. this step's table constants: wave-uniform, scalar loads
+    double cst[CST_COUNT];
+#pragma unroll
+    for (int i = 0; i < CST_COUNT; ++i) cst[i] = step_constant(s.tables, t, i);
+    // 3. the wave's actions tile, then the per-charger state
+    TileStage<KT, kWave> act_tile;
+    act_tile.issue(act + e0 * Ad, nw * Ad, vec_io != 0, lane);
+    uint32_t w[NC], auxh[NC];
+    double aux[NC], run[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
+        if (PK) {   // packed device-day record: word | float32 aux << 32 (sng_layout.h)
+            const uint64_t rec = bld(reinterpret_cast<const uint64_t *>(aux_t), el8, r8);
+            w[c] = (uint32_t)rec;
+            auxh[c] = (uint32_t)(rec >> 32);
+        } else {
+            w[c] = bld(word_t, el4, r4);
+            aux[c] = bld(aux_t, el8, r8);
+        }
+        run[c] = bld(s.soc, el8, r8);
+    }
+    act_tile.commit(s_act, lane);
+    wave_lds_fence();
+
+    const float *a_row = s_act + lane * Ad;
+    float *o_row = s_obs + lane * O;
+    float av[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) av[c] = a_row[c];
+    const float bess_action = p.bess ? a_row[NC] : 0.0f;
+    const int k_soc = p.pv ? 8 : 4;
+    // the header needs only the PV ratio and the constants: written while the chargers' loads fly
+    if (live) write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio, fpv, fpr);
+
+    double pwv[NC];
+    double pen_v = 0.0, seq_pos = 0.0, seq_neg = 0.0, pmin = __builtin_inf();
+    int n_pos = 0, n_neg = 0;
+    uint32_t n_nonexist = 0, fl = 0;
+    bool pos_other = false;   // a positive power that is not the float32 charging product
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            const uint32_t capi = (w[c] >> W_CAP_SHIFT) & 0xffu;
+            const double aux_c = PK ? (double)__uint_as_float(auxh[c]) : aux[c];
+            const ChargerResult r =
+                charger_step<true, true>(p, w[c], aux_c, run[c], req[c], av[c], t, recip_cap((double)capi));
+            bst<kNT>(s.soc, el8, r.soc, (uint32_t)c * (uint32_t)E * 8u);
+            o_row[k_soc + c] = (float)r.soc;
+            o_row[k_soc + NC + c] = departure_obs(w[c]);
+            n_nonexist += r.nx;
+            fl |= r.fl;
+            pen_v += r.q;
+            const double pw = r.pw;
+            pwv[c] = pw;
+            const bool ip = pw > 0.0;
+            seq_pos += __builtin_fmax(pw, 0.0);   // v_max/v_min drop a NaN power, as P[P > 0] does
+            seq_neg += __builtin_fmin(pw, 0.0);
+            n_pos += ip ? 1 : 0;
+            n_neg += (pw < 0.0) ? 1 : 0;
+            pmin = __builtin_fmin(pmin, ip ? pw : __builtin_inf());
+            pos_other |= ip && !(av[c] > 0.0f);
+#ifndef SNG_LEAN_NOSB
+            // chargers in order: charger c waits only for its own loads (vmcnt counts down charger
+            // by charger) while the later chargers' loads are in flight
+            __builtin_amdgcn_sched_barrier(0);
+#endif
+        }
+    }
+    double p_ch = seq_pos, p_dis = seq_neg;
+    if constexpr (NC >= 8) {
+        const bool pos_slow = n_pos >= 8 && (pos_other || !(seq_pos <= pmin * 0x1.0p28));
+        const bool slow = live && (pos_slow || n_neg >= 8);
+        if (__builtin_amdgcn_ballot_w64(slow)) {   // wave-uniform: rare
+            if (slow) {
+                double *row_pos = s_pos + lane * NC, *row_neg = s_neg + lane * NC;
+                int kp = 0, kn = 0;
+#pragma unroll
+                for (int c = 0; c < NC; ++c) {
+                    row_pos[kp] = pwv[c];
+                    row_neg[kn] = pwv[c];
+                    kp += (pwv[c] > 0.0) ? 1 : 0;
+                    kn += (pwv[c] < 0.0) ? 1 : 0;
+                }
+                p_ch = pairwise_row_c<NC>(row_pos, n_pos, seq_pos);
+                p_dis = pairwise_row_c<NC>(row_neg, n_neg, seq_neg);
+            }
+        }
+    }
+    if (live) {
+        // t = 0 reads the python index -1 slot (pen0); the per-charger terms are all 0 there
+        pen_v += (t == 0) ? pen0_l : 0.0;
+        env_tail<false>(p, s, info, e0, lo, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action, p_ch, p_dis,
+                        pen_v, 100.0 * (double)n_nonexist, fl, o_row, cst, fpv, fpr,
+                        info.episode_return ? ret_l : 0.0, 0.0, reward, done);
+    }
+    wave_lds_fence();
+    copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
+    (void)A;
 }
 
 // ---------------------------------------------------------------------------------
@@ -621,6 +773,13 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     double *s_neg = s_pos + (kRows ? WENVS * NC : 0);             // [WENVS][NC] compacted negative powers
     double *s_pw = s_neg + (kRows ? WENVS * NC : 0);              // [WENVS][NC] per-charger powers (L > 1)
     double *s_q = reinterpret_cast<double *>(s_act);              // [WENVS][NC] penalty terms (L > 1)
+#if !defined(SNG_LEAN_OFF) && !defined(SNG_STAMPS)
+    if constexpr (L == 1 && kRows && !DIAG && FAST) {
+        step_lean<NC, PK>(p, s, info, act, obs, reward, done, E, t, vec_io, s_act, s_obs, s_pos, s_neg, e0, nw, lane);
+        if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0) *s.episode += 1;   // see below
+        return;
+    }
+#endif
     const uint32_t *__restrict__ word = s.word;
     const double *__restrict__ auxv = s.aux;
     const double *__restrict__ reqv = s.req;
@@ -634,7 +793,7 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     // branch separates it from the per-charger loads, so the wait before the commits is
     // vmcnt(#per-charger loads) and charger c's update starts as soon as its own loads land.
     // Non-live lanes load a valid env (E - 1) and discard it.
-    const int64_t el = live ? e : (le < WENVS ? E - 1 : e0);   // idle lanes (SNG_V_HALF) read lane 0's lines
+    const int64_t el = live ? e : E - 1;
     const uint32_t lo = (uint32_t)(el - e0);   // lane offset from the wave's first env
     const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;   // byte offsets of the env
     const uint32_t *__restrict__ word_t = word + tbase * (size_t)E;   // this step's timeline planes
@@ -770,23 +929,6 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     double pen_v = 0.0;
     uint32_t n_nonexist = 0;
     uint32_t fl = 0;
-#if defined(SNG_V_NEGSKIP)
-    // Only a negative action makes a charger power negative (charger_step: moved && !chg), so a
-    // wavefront none of whose live envs has one skips the discharging total's accumulation: it is
-    // the empty sum, +0.0, as numpy's P[P < 0].sum() (charging_station.py:293).  Wave-uniform.
-    double pwv[kRows ? (NC > 0 ? NC : 1) : 1];
-    auto add_pos = [&](double pw) {
-        row_pos[n_pos] = pw;
-        seq_pos += __builtin_fmax(pw, 0.0);
-        n_pos += (pw > 0.0) ? 1 : 0;
-    };
-    bool neg_lane = false;
-    if (kRows && live) {
-#pragma unroll
-        for (int c = 0; c < (NC > 0 ? NC : 1); ++c) neg_lane |= a_row[c] < 0.0f;
-    }
-    const bool wave_neg = __builtin_amdgcn_ballot_w64(neg_lane) != 0;
-#endif
     if (live) {
         for (int c0 = cbeg; c0 < cend; c0 += CH) {
             if (c0 != cbeg) load_batch(c0);
@@ -818,21 +960,8 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                 n_nonexist += r.nx;
                 fl |= r.fl;
                 if (L == 1) {
-#if defined(SNG_V_REQCONST)
-                    if (!kRows) pen_v += r.q;   // kRows: the penalty terms are summed after the loop
-#else
                     pen_v += r.q;
-#endif
-#if defined(SNG_V_NEGSKIP)
-                    if (kRows) {
-                        pwv[j] = r.pw;   // the negative powers are compacted after the loop, if any
-                        add_pos(r.pw);
-                    } else {
-                        add_power(r.pw);
-                    }
-#else
                     add_power(r.pw);
-#endif
                 } else {
                     s_pw[le * NC + c] = r.pw;
                     s_q[le * NC + c] = r.q;
@@ -844,30 +973,6 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             }
         }
     }
-#if defined(SNG_V_NEGSKIP)
-    if (kRows && L == 1 && live && wave_neg) {
-#pragma unroll
-        for (int c = 0; c < (NC > 0 ? NC : 1); ++c) {
-            const double pw = pwv[c];
-            row_neg[n_neg] = pw;
-            seq_neg += __builtin_fmin(pw, 0.0);
-            n_neg += (pw < 0.0) ? 1 : 0;
-        }
-    }
-#endif
-#if defined(SNG_V_REQCONST)
-    // the penalty terms in charger order (Python's sum over the list, penaliser.py:55); without a
-    // requested-SoC stream Requested_SOC is the literal 1.0 (threshold 0.95), on a replayed day 0
-    if (kRows && L == 1 && live && t > 0 && !p.req_zero) {
-        if (!p.req_stream) {
-#pragma unroll
-            for (int c = 0; c < (NC > 0 ? NC : 1); ++c) pen_v += pen_term(w[c], run[c], 1.0);
-        } else {
-#pragma unroll
-            for (int c = 0; c < (NC > 0 ? NC : 1); ++c) pen_v += pen_term(w[c], run[c], req[c]);
-        }
-    }
-#endif
     if (L > 1) {
         // gather the env's lanes (same wavefront): counts and flag bits, then in-order
         // penalty / power sums by the leader from LDS
