@@ -25,7 +25,8 @@
 #include "sng_mt.h"
 
 namespace sng {
-hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
+hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
+                       const float *act, float *obs,
                        double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
                        hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
@@ -1043,7 +1044,7 @@ int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint
     if (env->t >= env->p.T) return fail(env, SNG_ERR_STATE, "the day is over: call reset()");
     HIP_TRY(env, hipSetDevice(env->device));
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
-    HIP_TRY(env, launch_step(env->p, env->ds, info_ptrs(info), actions, obs, reward, done, env->E, env->t, vec,
+    HIP_TRY(env, launch_step(env->p, env->ds, info_ptrs(info), env->host_tab, actions, obs, reward, done, env->E, env->t, vec,
                              as_stream(stream)));
     env->t += 1;
     if (env->t == env->p.T) env->day_finished = true;
@@ -1439,7 +1440,7 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
             e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, obs, ipd.episode_return, vec, cs);
         }
         for (int t = 0; e == hipSuccess && t < p.T; ++t)
-            e = launch_step(p, env->ds, ipd, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
+            e = launch_step(p, env->ds, ipd, env->host_tab, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, cs);
     }
     hipGraph_t graph = nullptr;
     hipError_t e2 = hipStreamEndCapture(cs, &graph);
@@ -1523,7 +1524,7 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
         e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, obs, ip.episode_return, vec, st);
         for (int t = 0; e == hipSuccess && t < T; ++t) {
             hipEvent_t a = ev[2 * ((size_t)d * T + t)], b = ev[2 * ((size_t)d * T + t) + 1];
-            e = launch_step(p, env->ds, ip, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, st, a, b);
+            e = launch_step(p, env->ds, ip, env->host_tab, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, st, a, b);
         }
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);

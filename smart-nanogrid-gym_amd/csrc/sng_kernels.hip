@@ -323,7 +323,7 @@ __device__ __forceinline__ double profile_factor(uint64_t env_seed, uint32_t dom
 // Per-step constants staged in LDS by the step kernel: irr_norm[t..t+3], price_norm[t..t+3],
 // pv_power[t], price[t].
 enum { CST_IRR = 0, CST_PN = 4, CST_PV = 8, CST_PRICE = 9, CST_COUNT = 10 };
-__device__ __forceinline__ double step_constant(const Tables *tb, int t, int i) {
+__host__ __device__ inline double step_constant(const Tables *tb, int t, int i) {
     return i < CST_PN ? tb->irr_norm[t + i]
                       : i < CST_PV ? tb->price_norm[t + i - CST_PN] : i == CST_PV ? tb->pv_power[t] : tb->price[t];
 }
@@ -576,83 +576,90 @@ __device__ __forceinline__ double recip_cap(double c) {
 }
 
 // ---------------------------------------------------------------------------------
-// The lean step: the one-lane, no-diagnostics, NumPy-2 / power-of-two-dt step of a station of
-// N <= 16 chargers (every configuration the bench and a training loop run), one wavefront per 64
-// envs.  Against the general kernel below it keeps nothing in LDS but the actions and observation
-// tiles: the step constants sit in scalar registers, 1/cap comes from recip_cap instead of an LDS
-// table (no per-wave table staging, no LDS round trip per charger), and the charging / discharging
-// totals are the running sums the lane keeps anyway whenever those equal numpy's pairwise sum of the
-// compacted arrays (charging_station.py:289-293) exactly:
-//   - fewer than 8 terms: numpy sums them sequentially (loops_utils.h.src), and the skipped +0.0
-//     terms leave a sum unchanged;
-//   - positive powers are float32 values (the NEP 50 product pc, charger.py:92-94, when charging);
-//     when the smallest of them, pmin, satisfies sum <= pmin * 2^28, every partial sum is a multiple
-//     of pmin's float32 ulp below 2^53 such ulps, so every addition is exact in any order.
-// Only a lane with 8 or more negative powers, or 8 or more positive ones whose sum is not provably
-// exact, compacts its powers into its LDS rows and runs the pairwise sum (rare; wave-uniform skip).
+// The lean step kernel: the one-lane, no-diagnostics, NumPy-2 / power-of-two-dt step of a station of
+// N <= 16 chargers without stochastic profiles (every configuration the bench and a training loop
+// run), one wavefront per 64 envs, 4 wavefronts per workgroup with wavefront-private LDS tiles.
+// Against the general step_kernel below:
+//   - the prologue is one kernarg round trip: no early exit (a wavefront past E loads env E - 1 and
+//     stores nothing), no runtime branch before the loads (the requested-SoC stream is the template
+//     argument REQ), and this step's table constants arrive by value (StepConst) instead of through
+//     the tables pointer, so every vector load issues right after the kernel arguments land;
+//   - nothing but the actions and observation tiles lives in LDS: 1/cap comes from recip_cap (no
+//     per-wavefront table staging, no LDS round trip per charger);
+//   - the charging / discharging totals are the running sums the lane keeps anyway whenever those
+//     equal numpy's pairwise sum of the compacted arrays (charging_station.py:289-293) exactly:
+//       * fewer than 8 terms: numpy sums them sequentially (loops_utils.h.src), and the skipped +0.0
+//         terms leave a sum unchanged;
+//       * positive powers are float32 values (the NEP 50 product pc, charger.py:92-94, when
+//         charging); when the smallest of them, pmin, satisfies sum <= pmin * 2^28, every partial sum
+//         is a multiple of pmin's float32 ulp below 2^53 such ulps, so every addition is exact in any
+//         order.
+//     Only a lane with 8 or more negative powers, or 8 or more positive ones whose sum is not
+//     provably exact, compacts its powers into its LDS rows and runs the pairwise sum (rare; skipped
+//     wave-uniformly otherwise).
 // ---------------------------------------------------------------------------------
-template <int NC, bool PK>
-__device__ __forceinline__ void step_lean(const Params &p, const DeviceState &s, const InfoPtrs &info,
-                                          const float *__restrict__ act, float *__restrict__ obs,
-                                          double *__restrict__ reward, uint8_t *__restrict__ done, int64_t E, int t,
-                                          int vec_io, float *s_act, float *s_obs, double *s_pos, double *s_neg,
-                                          int64_t e0, int nw, int lane) {
-    constexpr int A = NC + 1;   // with the BESS action; without a BESS the tile is one float narrower
-    constexpr int KT = ((NC + 1) * kWave + 4 * kWave - 1) / (4 * kWave);
+struct StepConst {
+    double v[CST_COUNT];   // step_constant(tables, t, i) for i < CST_COUNT
+};
+
+template <int NC>
+struct LeanLds {
+    static constexpr int A = NC + 1;   // actions per env with a BESS (one fewer without)
+    static constexpr int O = 2 * NC + 9;
+    static constexpr int ACT = round4(kWave * A), OBS = round4(kWave * O);
+    static constexpr size_t WAVE_BYTES = (size_t)(ACT + OBS) * 4 + (size_t)2 * kWave * NC * 8;
+    static constexpr size_t BYTES = 4 * WAVE_BYTES;
+};
+
+template <int NC, bool PK, bool REQ>
+__global__ __launch_bounds__(256) void step_lean_kernel(const float *__restrict__ act, float *__restrict__ obs,
+                                                        double *__restrict__ reward, uint8_t *__restrict__ done,
+                                                        int64_t E, int t, int vec_io, StepConst k, Params p,
+                                                        DeviceState s, InfoPtrs info) {
+    using Lay = LeanLds<NC>;
+    constexpr int KT = (Lay::A * kWave + 4 * kWave - 1) / (4 * kWave);
+    extern __shared__ __attribute__((aligned(16))) float lds[];
     const int Ad = p.act_dim, O = p.obs_dim;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const int64_t e0 = (int64_t)blockIdx.x * 256 + (int64_t)wave * kWave;
+    const int64_t rem_e = E - e0;
+    const int nw = rem_e <= 0 ? 0 : (rem_e < kWave ? (int)rem_e : kWave);
     const bool live = lane < nw;
+    float *s_act = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + wave * Lay::WAVE_BYTES);
+    float *s_obs = s_act + Lay::ACT;
+    double *s_pos = reinterpret_cast<double *>(s_obs + Lay::OBS);
+    double *s_neg = s_pos + kWave * NC;
     const int64_t el = live ? e0 + lane : E - 1;   // idle lanes load a valid env and discard it
-    const uint32_t lo = (uint32_t)(el - e0);
+    const int64_t ew = nw > 0 ? e0 : E - 1;         // a wavefront past E stages env E - 1's row
     const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;
     const size_t plane = (size_t)t * NC * (size_t)E;   // this step's timeline planes
-    const uint32_t *__restrict__ word_t = s.word + plane;
-    const double *__restrict__ aux_t = s.aux + plane;
-    const double *__restrict__ req_t = s.req + plane;
 
-    // 1. per-env values (pointer selects rather than branches: a disabled stream re-reads ratio)
-    const double ratio = bld(s.ratio, el8);
-    const double bess_l = bld(p.bess ? s.bess : s.ratio, el8);
+    // loads oldest-needed-first, all behind the one kernarg wait: the wave's actions tile and the
+    // per-env values (the LDS commit and the observation header wait for them, before any charger),
+    // then the per-charger state, which charger c waits for in order
+    TileStage<KT, kWave> act_tile;
+    act_tile.issue(act + ew * Ad, (nw > 0 ? nw : 1) * Ad, vec_io != 0, lane);
+    const double ratio = bld(s.ratio, el8);   // pointer selects rather than branches: a disabled
+    const double bess_l = bld(p.bess ? s.bess : s.ratio, el8);   // stream re-reads ratio
     const double pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
     const double ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
-    double req[NC];
-    if (p.req_stream && !p.req_zero) {
-#pragma unroll
-        for (int c = 0; c < NC; ++c) req[c] = bld(req_t, el8, (uint32_t)c * (uint32_t)E * 8u);
-    } else {   // no stream: 1.0 (charging_station.py:230-232); a replayed day: the cleared 0.0
-        const double rq = p.req_zero ? 0.0 : 1.0;
-#pragma unroll
-        for (int c = 0; c < NC; ++c) req[c] = rq;
-    }
-    double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
-    if (p.noise) {
-        const size_t pl = (size_t)(p.T + 3) * E;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            fpv[j] = bld(s.prof + (size_t)(t + j) * E, el8);
-            fpr[j] = bld(s.prof + pl + (size_t)(t + j) * E, el8);
-        }
-    }
-    // 2. this step's table constants: wave-uniform, scalar loads
-    double cst[CST_COUNT];
-#pragma unroll
-    for (int i = 0; i < CST_COUNT; ++i) cst[i] = step_constant(s.tables, t, i);
-    // 3. the wave's actions tile, then the per-charger state
-    TileStage<KT, kWave> act_tile;
-    act_tile.issue(act + e0 * Ad, nw * Ad, vec_io != 0, lane);
     uint32_t w[NC], auxh[NC];
-    double aux[NC], run[NC];
+    double aux[NC], run[NC], req[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
         if (PK) {   // packed device-day record: word | float32 aux << 32 (sng_layout.h)
-            const uint64_t rec = bld(reinterpret_cast<const uint64_t *>(aux_t), el8, r8);
+            const uint64_t rec = bld(reinterpret_cast<const uint64_t *>(s.aux + plane), el8, r8);
             w[c] = (uint32_t)rec;
             auxh[c] = (uint32_t)(rec >> 32);
         } else {
-            w[c] = bld(word_t, el4, r4);
-            aux[c] = bld(aux_t, el8, r8);
+            w[c] = bld(s.word + plane, el4, r4);
+            aux[c] = bld(s.aux + plane, el8, r8);
         }
         run[c] = bld(s.soc, el8, r8);
+        // Requested_SOC[c, t-1]; without the stream 1.0 (charging_station.py:230-232), or the cleared
+        // 0.0 of a replayed day (Params::req_zero)
+        req[c] = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
     }
     act_tile.commit(s_act, lane);
     wave_lds_fence();
@@ -664,8 +671,9 @@ __device__ __forceinline__ void step_lean(const Params &p, const DeviceState &s,
     for (int c = 0; c < NC; ++c) av[c] = a_row[c];
     const float bess_action = p.bess ? a_row[NC] : 0.0f;
     const int k_soc = p.pv ? 8 : 4;
+    const double one4[4] = {1.0, 1.0, 1.0, 1.0};
     // the header needs only the PV ratio and the constants: written while the chargers' loads fly
-    if (live) write_obs_header(o_row, p, cst + CST_IRR, cst + CST_PN, ratio, fpv, fpr);
+    if (live) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, one4, one4);
 
     double pwv[NC];
     double pen_v = 0.0, seq_pos = 0.0, seq_neg = 0.0, pmin = __builtin_inf();
@@ -724,13 +732,16 @@ __device__ __forceinline__ void step_lean(const Params &p, const DeviceState &s,
     if (live) {
         // t = 0 reads the python index -1 slot (pen0); the per-charger terms are all 0 there
         pen_v += (t == 0) ? pen0_l : 0.0;
-        env_tail<false>(p, s, info, e0, lo, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action, p_ch, p_dis,
-                        pen_v, 100.0 * (double)n_nonexist, fl, o_row, cst, fpv, fpr,
+        env_tail<false>(p, s, info, e0, (uint32_t)lane, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action,
+                        p_ch, p_dis, pen_v, 100.0 * (double)n_nonexist, fl, o_row, k.v, one4, one4,
                         info.episode_return ? ret_l : 0.0, 0.0, reward, done);
     }
     wave_lds_fence();
-    copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
-    (void)A;
+    if (nw > 0) copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
+    // a device-RNG day's first step advances the day counter its reset read (generate_kernel); no-return
+    // atomic, so nothing waits for it.  A replayed day (bump_day = 0) drew no counter value of its own.
+    if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_fetch_add(s.episode, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------
@@ -773,13 +784,6 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     double *s_neg = s_pos + (kRows ? WENVS * NC : 0);             // [WENVS][NC] compacted negative powers
     double *s_pw = s_neg + (kRows ? WENVS * NC : 0);              // [WENVS][NC] per-charger powers (L > 1)
     double *s_q = reinterpret_cast<double *>(s_act);              // [WENVS][NC] penalty terms (L > 1)
-#if !defined(SNG_LEAN_OFF) && !defined(SNG_STAMPS)
-    if constexpr (L == 1 && kRows && !DIAG && FAST) {
-        step_lean<NC, PK>(p, s, info, act, obs, reward, done, E, t, vec_io, s_act, s_obs, s_pos, s_neg, e0, nw, lane);
-        if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0) *s.episode += 1;   // see below
-        return;
-    }
-#endif
     const uint32_t *__restrict__ word = s.word;
     const double *__restrict__ auxv = s.aux;
     const double *__restrict__ reqv = s.req;
@@ -1378,6 +1382,44 @@ struct LaunchEvents {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 
+// The lean step kernel's configurations: a compile-time station of N <= 16, one lane per env, no
+// diagnostics, NumPy-2 promotion with a power-of-two dt, no stochastic profiles.
+static bool lean_step(const Params &p, bool diag) {
+    const bool nc = p.n == 1 || p.n == 2 || p.n == 4 || p.n == 8 || p.n == 10 || p.n == 16;
+    return nc && !diag && !p.legacy && p.dt_pow2 && !p.noise && !(p.lanes == 2 || p.lanes == 4);
+}
+
+template <int NC>
+static void launch_lean(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
+                        const float *act, float *obs, double *reward, uint8_t *done, int64_t E, int t, int vec_io,
+                        hipStream_t stream, const LaunchEvents *ev) {
+    StepConst k;
+    for (int i = 0; i < CST_COUNT; ++i) k.v[i] = step_constant(&tab, t, i);
+    const bool req = p.req_stream && !p.req_zero;
+    auto kern = p.packed ? (req ? step_lean_kernel<NC, true, true> : step_lean_kernel<NC, true, false>)
+                         : (req ? step_lean_kernel<NC, false, true> : step_lean_kernel<NC, false, false>);
+    const dim3 grid((unsigned)((E + 255) / 256)), block(256);
+    const uint32_t lds = (uint32_t)LeanLds<NC>::BYTES;
+    if (ev)
+        hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,
+                              vec_io, k, p, s, info);
+    else
+        hipLaunchKernelGGL(kern, grid, block, lds, stream, act, obs, reward, done, E, t, vec_io, k, p, s, info);
+}
+
+static void launch_lean_n(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
+                          const float *act, float *obs, double *reward, uint8_t *done, int64_t E, int t, int vec_io,
+                          hipStream_t stream, const LaunchEvents *ev) {
+    switch (p.n) {
+        case 1: launch_lean<1>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 2: launch_lean<2>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 4: launch_lean<4>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 8: launch_lean<8>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        case 10: launch_lean<10>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+        default: launch_lean<16>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev); break;
+    }
+}
+
 template <int NC, int L, bool DIAG>
 static void launch_step_t(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
                           double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
@@ -1441,11 +1483,17 @@ static bool info_diag(const InfoPtrs &info) {
            info.bess_calc_power || info.nonexistent || info.bess_initial || info.charger_power || info.vehicle_soc;
 }
 
-hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const float *act, float *obs,
-                       double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
-                       hipEvent_t ev_start, hipEvent_t ev_stop) {
+hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
+                       const float *act, float *obs, double *reward, uint8_t *done, int64_t E, int t, int vec_io,
+                       hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
     LaunchEvents evs{ev_start, ev_stop};
     const LaunchEvents *ev = (ev_start && ev_stop) ? &evs : nullptr;
+#if !defined(SNG_LEAN_OFF) && !defined(SNG_STAMPS)
+    if (lean_step(p, info_diag(info))) {
+        launch_lean_n(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
+        return hipGetLastError();
+    }
+#endif
     if (info_diag(info))
         launch_step_n<true>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev);
     else
@@ -1456,6 +1504,11 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
 // The name rocprofv3 reports for the step kernel launch_step would dispatch next (the template
 // arguments launch_step_n / launch_step_l / launch_step_t select).
 int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) {
+#if !defined(SNG_LEAN_OFF) && !defined(SNG_STAMPS)
+    if (lean_step(p, info_diag(info)))
+        return snprintf(buf, (size_t)len, "void sng::step_lean_kernel<%d, %s, %s>", p.n, p.packed ? "true" : "false",
+                        (p.req_stream && !p.req_zero) ? "true" : "false");
+#endif
     int nc = 0, lanes = 1;
     switch (p.n) {
         case 2: case 4: case 8: case 10: case 16: case 50:

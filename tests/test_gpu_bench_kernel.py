@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 
 from smart_nanogrid_gym import SmartNanogridVecEnv  # noqa: E402
 
-BENCH_KERNEL = "void sng::step_kernel<10, 1, false, true, true>"
+BENCH_KERNEL = "void sng::step_lean_kernel<10, true, false>"
 KW = dict(number_of_chargers=10, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse",
           pv_system_available_in_model=True, battery_system_available_in_model=True)
 
