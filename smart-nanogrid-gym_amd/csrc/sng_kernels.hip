@@ -41,9 +41,15 @@ __device__ unsigned long long *g_stamps;
         const unsigned long long ts_ = __builtin_amdgcn_s_memrealtime();                             \
         if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 4 + (k)] = ts_;              \
     } while (0)
+// The lean step kernel's stamps take no wait of their own: s_memrealtime when the wavefront reaches the
+// point, kept in registers and written by workgroup 0's first lane at the end -> g_stamps[block*8 + k].
+#define SNG_LSTAMP(k) stamp_[k] = __builtin_amdgcn_s_memrealtime()
 #else
 #define SNG_STAMP(k) \
     do {             \
+    } while (0)
+#define SNG_LSTAMP(k) \
+    do {              \
     } while (0)
 #endif
 
@@ -619,6 +625,10 @@ __global__ __launch_bounds__(256) void step_lean_kernel(const float *__restrict_
     using Lay = LeanLds<NC>;
     constexpr int KT = (Lay::A * kWave + 4 * kWave - 1) / (4 * kWave);
     extern __shared__ __attribute__((aligned(16))) float lds[];
+#ifdef SNG_STAMPS
+    unsigned long long stamp_[5];
+#endif
+    SNG_LSTAMP(0);
     const int Ad = p.act_dim, O = p.obs_dim;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const int64_t e0 = (int64_t)blockIdx.x * 256 + (int64_t)wave * kWave;
@@ -663,6 +673,7 @@ __global__ __launch_bounds__(256) void step_lean_kernel(const float *__restrict_
     }
     act_tile.commit(s_act, lane);
     wave_lds_fence();
+    SNG_LSTAMP(1);
 
     const float *a_row = s_act + lane * Ad;
     float *o_row = s_obs + lane * O;
@@ -709,6 +720,7 @@ __global__ __launch_bounds__(256) void step_lean_kernel(const float *__restrict_
 #endif
         }
     }
+    SNG_LSTAMP(2);
     double p_ch = seq_pos, p_dis = seq_neg;
     if constexpr (NC >= 8) {
         const bool pos_slow = n_pos >= 8 && (pos_other || !(seq_pos <= pmin * 0x1.0p28));
@@ -737,7 +749,13 @@ __global__ __launch_bounds__(256) void step_lean_kernel(const float *__restrict_
                         info.episode_return ? ret_l : 0.0, 0.0, reward, done);
     }
     wave_lds_fence();
+    SNG_LSTAMP(3);
     if (nw > 0) copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
+    SNG_LSTAMP(4);
+#ifdef SNG_STAMPS
+    if (threadIdx.x == 0 && g_stamps)
+        for (int i = 0; i < 5; ++i) g_stamps[(size_t)blockIdx.x * 8 + i] = stamp_[i];
+#endif
     // a device-RNG day's first step advances the day counter its reset read (generate_kernel); no-return
     // atomic, so nothing waits for it.  A replayed day (bump_day = 0) drew no counter value of its own.
     if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0)
@@ -1488,7 +1506,7 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
                        hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
     LaunchEvents evs{ev_start, ev_stop};
     const LaunchEvents *ev = (ev_start && ev_stop) ? &evs : nullptr;
-#if !defined(SNG_LEAN_OFF) && !defined(SNG_STAMPS)
+#if !defined(SNG_LEAN_OFF)
     if (lean_step(p, info_diag(info))) {
         launch_lean_n(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
         return hipGetLastError();
@@ -1504,7 +1522,7 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
 // The name rocprofv3 reports for the step kernel launch_step would dispatch next (the template
 // arguments launch_step_n / launch_step_l / launch_step_t select).
 int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) {
-#if !defined(SNG_LEAN_OFF) && !defined(SNG_STAMPS)
+#if !defined(SNG_LEAN_OFF)
     if (lean_step(p, info_diag(info)))
         return snprintf(buf, (size_t)len, "void sng::step_lean_kernel<%d, %s, %s>", p.n, p.packed ? "true" : "false",
                         (p.req_stream && !p.req_zero) ? "true" : "false");

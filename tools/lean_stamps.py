@@ -1,0 +1,64 @@
+"""Per-workgroup phase timeline of the lean step kernel (diagnostic build libsng_stamps.so).
+
+    make -C smart-nanogrid-gym_amd/csrc stamps
+    SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so python tools/lean_stamps.py
+
+The lean kernel's stamps add no wait of their own (s_memrealtime, 100 MHz, when the first wavefront of a
+workgroup reaches the point): 0 = start, 1 = actions tile staged (the tile and the per-env values landed),
+2 = chargers done, 3 = env tail done (observation tile complete), 4 = observation stores issued.  The
+kernel's device time per step comes from the HIP-event probe of the same process, so the stretch after
+stamp 4 (store drain + end of kernel) is that time minus the last stamp.
+"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "smart-nanogrid-gym_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from smart_nanogrid_gym import SmartNanogridVecEnv, _native  # noqa: E402
+
+
+def main():
+    L = _native.lib()
+    setter = getattr(L, "sng_debug_set_stamps")
+    setter.argtypes = [ctypes.c_void_p]
+    E, N = int(os.environ.get("ENVS", 65536)), 10
+    venv = SmartNanogridVecEnv(E, seed=3, rng="device", number_of_chargers=N, time_interval="1h",
+                               charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+    venv._info.flags = None
+    print("kernel:", venv.step_kernel_name())
+    blocks = (E + 255) // 256
+    buf = torch.zeros(blocks * 8, dtype=torch.int64, device="cuda:0")
+    assert setter(ctypes.c_void_p(buf.data_ptr())) == 0
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    acts = torch.rand((24, E, N + 1), device="cuda:0", generator=g)
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    acts = torch.where(torch.rand(acts.shape, device="cuda:0", generator=g) < 0.2, torch.zeros_like(acts), acts)
+    rows = []
+    for day in range(3):
+        venv.reset_tensors()
+        for t in range(24):
+            venv.step_tensors(acts[t])
+            torch.cuda.synchronize()
+            if day > 0:
+                rows.append(buf.view(blocks, 8)[:, :5].cpu().numpy().astype(np.float64) * 10.0)   # ns
+    ph = np.stack(rows)                      # [steps, blocks, 5]
+    ph = ph - ph[..., :1].min(axis=1, keepdims=True)
+    q = lambda x: f"med {np.median(x) / 1e3:6.3f}  p10 {np.percentile(x, 10) / 1e3:6.3f}  p90 {np.percentile(x, 90) / 1e3:6.3f} us"
+    names = ["start (rel. first WG)", "tile + per-env landed", "chargers", "env tail", "obs stores issued"]
+    print(f"{'wave start':28s}", q(ph[..., 0]))
+    for k in range(1, 5):
+        print(f"{names[k]:28s}", q(ph[..., k] - ph[..., k - 1]))
+    print(f"{'last WG reaches stamp 4':28s}", q(ph[..., 4].max(axis=1)))
+    ms = venv.time_step_kernels(acts, days=1)
+    print(f"HIP-event step time: mean {np.mean(ms) * 1e3:.3f} us")
+    setter(ctypes.c_void_p(0))
+    venv.close()
+
+
+if __name__ == "__main__":
+    main()
