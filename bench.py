@@ -123,8 +123,9 @@ def load_pmc_traffic(n_envs, chargers, kernel):
         return None
     try:
         d = json.load(open(path))
-        if d.get("envs") == n_envs and d.get("chargers") == chargers and d.get("kernel") == kernel:
-            return d.get("bytes_per_launch")
+        for e in (d if isinstance(d, list) else [d]):
+            if e.get("envs") == n_envs and e.get("chargers") == chargers and e.get("kernel") == kernel:
+                return e.get("bytes_per_launch")
     except Exception:
         return None
     return None

@@ -222,7 +222,9 @@ int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint
              const SngInfo *info, void *stream);
 
 /* The kernel name (as rocprofv3 reports it) of the step kernel sng_step would launch next with this
- * `info` (NULL allowed): "void sng::step_kernel<NC, L, DIAG, FAST, PK>". */
+ * `info` (NULL allowed): "void sng::step_lean_kernel<N, PK, REQ>" for stations of N in {1,2,4,8,10,16}
+ * chargers stepped with one lane per env, no diagnostics, NumPy-2 promotion, a power-of-two dt,
+ * bounded charging and no stochastic profiles; "void sng::step_kernel<NC, L, DIAG, FAST, PK>" otherwise. */
 int sng_step_kernel_name(const SngEnv *env, const SngInfo *info, char *buf, int32_t len);
 
 /* Sticky per-env error flags (SNG_FLAG_*), copied to host after the work queued on `stream`;

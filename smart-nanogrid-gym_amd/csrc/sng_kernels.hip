@@ -608,17 +608,25 @@ struct StepConst {
     double v[CST_COUNT];   // step_constant(tables, t, i) for i < CST_COUNT
 };
 
+// Threads per workgroup of the lean step kernel: one wavefront (1,024 workgroups at E = 65,536).
+// A/B on one box (day of 65,536 x 10): 64 threads 6.33-6.38 us per step, 256 threads 6.47-6.55,
+// 128 threads 7.13-7.14 (tools/gpu_session.sh ablib).
+#ifndef SNG_LEAN_BLOCK
+#define SNG_LEAN_BLOCK 64
+#endif
+constexpr int kLeanBlock = SNG_LEAN_BLOCK;
+
 template <int NC>
 struct LeanLds {
     static constexpr int A = NC + 1;   // actions per env with a BESS (one fewer without)
     static constexpr int O = 2 * NC + 9;
     static constexpr int ACT = round4(kWave * A), OBS = round4(kWave * O);
     static constexpr size_t WAVE_BYTES = (size_t)(ACT + OBS) * 4 + (size_t)2 * kWave * NC * 8;
-    static constexpr size_t BYTES = 4 * WAVE_BYTES;
+    static constexpr size_t BYTES = (kLeanBlock / kWave) * WAVE_BYTES;
 };
 
 template <int NC, bool PK, bool REQ>
-__global__ __launch_bounds__(256) void step_lean_kernel(const float *__restrict__ act, float *__restrict__ obs,
+__global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__restrict__ act, float *__restrict__ obs,
                                                         double *__restrict__ reward, uint8_t *__restrict__ done,
                                                         int64_t E, int t, int vec_io, StepConst k, Params p,
                                                         DeviceState s, InfoPtrs info) {
@@ -631,7 +639,7 @@ __global__ __launch_bounds__(256) void step_lean_kernel(const float *__restrict_
     SNG_LSTAMP(0);
     const int Ad = p.act_dim, O = p.obs_dim;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
-    const int64_t e0 = (int64_t)blockIdx.x * 256 + (int64_t)wave * kWave;
+    const int64_t e0 = (int64_t)blockIdx.x * kLeanBlock + (int64_t)wave * kWave;
     const int64_t rem_e = E - e0;
     const int nw = rem_e <= 0 ? 0 : (rem_e < kWave ? (int)rem_e : kWave);
     const bool live = lane < nw;
@@ -1416,7 +1424,7 @@ static void launch_lean(const Params &p, const DeviceState &s, const InfoPtrs &i
     const bool req = p.req_stream && !p.req_zero;
     auto kern = p.packed ? (req ? step_lean_kernel<NC, true, true> : step_lean_kernel<NC, true, false>)
                          : (req ? step_lean_kernel<NC, false, true> : step_lean_kernel<NC, false, false>);
-    const dim3 grid((unsigned)((E + 255) / 256)), block(256);
+    const dim3 grid((unsigned)((E + kLeanBlock - 1) / kLeanBlock)), block(kLeanBlock);
     const uint32_t lds = (uint32_t)LeanLds<NC>::BYTES;
     if (ev)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,

@@ -4,7 +4,9 @@
 
 Reads <out>/prof/run_kernel_stats.csv (--kernel-trace --stats) and the two PMC passes
 <out>/pmc_fetch/run_counter_collection.csv (FETCH_SIZE) and <out>/pmc_write/... (WRITE_SIZE),
-writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.csv and profiles/pmc_step_kernel.json.
+writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.csv and an entry of
+profiles/pmc_step_kernel.json; the same for config 5 from prof_cfg5/, pmc5_fetch/ and pmc5_write/
+(profiles/<tag>_kernel_stats_config5.csv, profiles/<tag>_pmc_config5.csv).
 
 HBM bytes per launch (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE counts half the bytes of a coalesced streaming read, so
@@ -34,28 +36,43 @@ def main():
     out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out")
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
-    shutil.copyfile(os.path.join(out, "prof", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
-    fetch, nf = per_kernel(os.path.join(out, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
-    write, nw = per_kernel(os.path.join(out, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
-    rows = []
-    for k in sorted(set(fetch) | set(write)):
-        if "sng::" not in k:
+    meta_path = os.path.join(prof, "pmc_step_kernel.json")
+    try:
+        entries = json.load(open(meta_path))
+        entries = entries if isinstance(entries, list) else [entries]
+    except (OSError, ValueError):
+        entries = []
+    # (pass prefix, file suffix, envs, chargers): the headline workload and config 5
+    for pre, suf, envs, chargers in (("", "", 65536, 10), ("pmc5_", "_config5", 65536, 50)):
+        stats = os.path.join(out, "prof" + ("_cfg5" if suf else ""), "run_kernel_stats.csv")
+        fpath = os.path.join(out, (pre or "pmc_") + "fetch", "run_counter_collection.csv")
+        wpath = os.path.join(out, (pre or "pmc_") + "write", "run_counter_collection.csv")
+        if os.path.exists(stats):
+            shutil.copyfile(stats, os.path.join(prof, f"{tag}_kernel_stats{suf}.csv"))
+        if not (os.path.exists(fpath) and os.path.exists(wpath)):
             continue
-        f, w = fetch.get(k, 0.0), write.get(k, 0.0)
-        rows.append(dict(kernel=k.split("(")[0], dispatches=nf.get(k, 0), fetch_kib=round(f, 1), write_kib=round(w, 1),
-                         hbm_bytes_per_launch=int(2 * f * 1024 + w * 1024)))
-    with open(os.path.join(prof, f"{tag}_pmc.csv"), "w", newline="") as fp:
-        wr = csv.DictWriter(fp, fieldnames=list(rows[0]))
-        wr.writeheader()
-        wr.writerows(rows)
-    step = [r for r in rows if "step_kernel" in r["kernel"]][0]
-    meta = dict(source=f"profiles/{tag}_pmc.csv (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes)",
-                kernel=step["kernel"], envs=65536, chargers=10, bytes_per_launch=step["hbm_bytes_per_launch"],
-                fetch_kib=step["fetch_kib"], write_kib=step["write_kib"],
-                correction="traffic = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts half of streamed reads)")
-    json.dump(meta, open(os.path.join(prof, "pmc_step_kernel.json"), "w"), indent=1)
-    for r in rows:
-        print(r)
+        fetch, nf = per_kernel(fpath, "FETCH_SIZE")
+        write, nw = per_kernel(wpath, "WRITE_SIZE")
+        rows = []
+        for k in sorted(set(fetch) | set(write)):
+            if "sng::" not in k:
+                continue
+            f, w = fetch.get(k, 0.0), write.get(k, 0.0)
+            rows.append(dict(kernel=k.split("(")[0], dispatches=nf.get(k, 0), fetch_kib=round(f, 1),
+                             write_kib=round(w, 1), hbm_bytes_per_launch=int(2 * f * 1024 + w * 1024)))
+        with open(os.path.join(prof, f"{tag}_pmc{suf}.csv"), "w", newline="") as fp:
+            wr = csv.DictWriter(fp, fieldnames=list(rows[0]))
+            wr.writeheader()
+            wr.writerows(rows)
+        step = [r for r in rows if "step_" in r["kernel"]][0]
+        meta = dict(source=f"profiles/{tag}_pmc{suf}.csv (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes)",
+                    kernel=step["kernel"], envs=envs, chargers=chargers, bytes_per_launch=step["hbm_bytes_per_launch"],
+                    fetch_kib=step["fetch_kib"], write_kib=step["write_kib"],
+                    correction="traffic = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts half of streamed reads)")
+        entries = [e for e in entries if not (e.get("envs") == envs and e.get("chargers") == chargers)] + [meta]
+        for r in rows:
+            print(r)
+    json.dump(entries, open(meta_path, "w"), indent=1)
 
 
 if __name__ == "__main__":
