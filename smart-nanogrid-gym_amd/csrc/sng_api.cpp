@@ -36,6 +36,9 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
                            hipStream_t stream);
 hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream);
 hipError_t launch_bump_day(const DeviceState &s, hipStream_t stream);
+hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream);
+hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
+                          int i1, hipStream_t stream);
 int step_lanes_supported(int n, int lanes);
 int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len);
 }  // namespace sng
@@ -46,7 +49,6 @@ namespace {
 
 thread_local std::string g_create_error;
 
-constexpr int kMaxVehicles = 32;
 
 // numpy pairwise_sum (contiguous float64), used by ndarray.mean() in
 // PVSystemManager.calculate_solar_irradiance_mean (pv_system_manager.py:34-44)
@@ -374,8 +376,11 @@ struct SngEnv {
     uint32_t *h_word = nullptr;
     double *h_aux = nullptr, *h_req = nullptr, *h_ratio = nullptr, *h_pen0 = nullptr;
     hipEvent_t staging_done = nullptr;
-    // reference RNG streams, one numpy + one python MT19937 per env (allocated on first use)
-    std::vector<MT19937> np_rng, py_rng;
+    // reference RNG streams of every env (allocated on first use): numpy's on the device (RefStreams,
+    // drawn by ref_day_kernel), Python's on the host (two or three draws a day)
+    RefStreams rs{};
+    bool np_seeded = false;
+    std::vector<MT19937> py_rng;
     std::string err;
 
     size_t timeline() const { return (size_t)p.T * p.n * (size_t)E; }
@@ -466,17 +471,25 @@ int ensure_staging(SngEnv *env, bool with_req) {
     return SNG_OK;
 }
 
-// The reference's global RNG streams of every env: np.random.seed(s) and random.seed(s) with
-// s = seed + global env index (SngRngMode SNG_RNG_REFERENCE).
+// The reference's global RNG streams of every env, np.random.seed(s) and random.seed(s) with
+// s = seed + global env index (SngRngMode SNG_RNG_REFERENCE): Python's on the host ...
 void ensure_streams(SngEnv *env) {
-    if (!env->np_rng.empty()) return;
-    env->np_rng.resize(env->E);
+    if (!env->py_rng.empty()) return;
     env->py_rng.resize(env->E);
-    for (int64_t i = 0; i < env->E; ++i) {
-        const uint64_t s = env->seed + (uint64_t)env->p.env_offset + (uint64_t)i;
-        env->np_rng[i].seed_numpy((uint32_t)s);
-        env->py_rng[i].seed_python(s);
+    for (int64_t i = 0; i < env->E; ++i) env->py_rng[i].seed_python(env->seed + (uint64_t)env->p.env_offset + (uint64_t)i);
+}
+
+// ... and numpy's on the device (mt_seed_kernel), queued on `st`.
+int ensure_np_streams(SngEnv *env, hipStream_t st) {
+    if (!env->rs.mt) {
+        HIP_TRY(env, hipMalloc(&env->rs.mt, (size_t)env->E * 2 * kMtN * sizeof(uint32_t)));
+        HIP_TRY(env, hipMalloc(&env->rs.pos, (size_t)env->E * sizeof(int32_t)));
     }
+    if (!env->np_seeded) {
+        HIP_TRY(env, launch_ref_seed(env->rs, env->seed + (uint64_t)env->p.env_offset, env->E, st));
+        env->np_seeded = true;
+    }
+    return SNG_OK;
 }
 
 // Per-thread scratch for one env's day in the reference layout.
@@ -837,7 +850,7 @@ void sng_destroy(SngEnv *env) {
     (void)hipSetDevice(env->device);
     DeviceState &ds = env->ds;
     void *dev[] = {ds.soc, ds.bess, ds.bess0, ds.ratio, ds.pen0, ds.word, ds.aux, ds.req, ds.flags, ds.prof,
-                   ds.episode, env->d_tables};
+                   ds.episode, env->d_tables, env->rs.mt, env->rs.pos};
     for (void *x : dev)
         if (x) (void)hipFree(x);
     void *host[] = {env->h_word, env->h_aux, env->h_req, env->h_ratio, env->h_pen0};
@@ -864,7 +877,7 @@ int sng_get_timestep(const SngEnv *env) { return env ? env->t : -1; }
 int sng_set_env_offset(SngEnv *env, int64_t offset) {
     if (!env || offset < 0) return fail(env, SNG_ERR_INVALID_ARGUMENT, "bad env offset");
     env->p.env_offset = offset;
-    env->np_rng.clear();   // reference streams are re-seeded (seed + offset + i) at the next reset
+    env->np_seeded = false;   // reference streams are re-seeded (seed + offset + i) at the next reset
     env->py_rng.clear();
     env->day_finished = false;
     return SNG_OK;
@@ -875,7 +888,7 @@ int sng_set_seed(SngEnv *env, uint64_t seed, void *stream) {
     HIP_TRY(env, hipSetDevice(env->device));
     env->seed = seed;
     env->p.seed = seed;
-    env->np_rng.clear();   // re-seeded (seed + offset + i) at the next reset
+    env->np_seeded = false;   // re-seeded (seed + offset + i) at the next reset
     env->py_rng.clear();
     env->day_finished = false;
     env->replays = 0;
@@ -914,31 +927,27 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     }
     if (rng_mode != SNG_RNG_REFERENCE) return fail(env, SNG_ERR_INVALID_ARGUMENT, "unknown rng_mode");
 
-    const int N = env->p.n, T = env->p.T, S = env->slots;
+    // the day on the device (ref_day_kernel: numpy's stream, draw for draw); the PV ratio from each
+    // env's Python stream on the host, after the day-end draw the last step still owes
+    // (smart_nanogrid_environment.py:181, 349)
     ensure_streams(env);
+    int rc = ensure_np_streams(env, st);
+    if (rc) return rc;
     const bool with_req = env->p.req_enabled != 0;
     if (with_req) {
-        int rc = ensure_req(env);
+        rc = ensure_req(env);
         if (rc) return rc;
     }
-    int rc = ensure_staging(env, with_req);
+    rc = ensure_staging(env, false);
     if (rc) return rc;
+    env->p.req_stream = with_req ? 1 : 0;
+    HIP_TRY(env, launch_ref_day(env->p, env->ds, env->rs, env->E, env->i4, env->i10, env->i1, st));
     const bool end_draw = env->day_finished;
-    bool need = false;
-    rc = build_and_upload(env, with_req ? 1 : 0, st, &need,
-                          [&](int64_t i, DayScratch &sc, bool *nr, std::string &e) -> bool {
-                              DayView d = sc.view(N, S, kMaxVehicles);
-                              // the day-end draw of the previous step (smart_nanogrid_environment.py:181)
-                              if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
-                              if (!generate_day(env->cfg, T, env->np_rng[i], d)) {
-                                  e = "more vehicles per charger than supported";
-                                  return false;
-                              }
-                              env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;   // :349
-                              return encode_day(env->p, env->E, i, d, env->h_word, env->h_aux,
-                                                with_req ? env->h_req : nullptr, &env->h_pen0[i], nr, e);
-                          });
-    if (rc) return rc;
+    for (int64_t i = 0; i < env->E; ++i) {
+        if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
+        env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;
+    }
+    std::fill(env->h_pen0, env->h_pen0 + env->E, 0.0);   // python index -1 of a generated day holds zeros
     rc = finish_host_day(env, with_req, obs, st);
     if (rc) return rc;
     env->gen_mode = SNG_RNG_REFERENCE;
@@ -1276,7 +1285,7 @@ static StateHeader state_layout(const SngEnv *env, bool with_return) {
     h.has_req = (env->ds.req && env->p.req_stream) ? 1 : 0;
     h.has_prof = env->ds.prof ? 1 : 0;
     h.has_return = with_return ? 1 : 0;
-    h.has_streams = env->np_rng.empty() ? 0 : 1;
+    h.has_streams = env->py_rng.empty() ? 0 : 1;
     const size_t E = (size_t)env->E, tl = env->timeline();
     size_t b = sizeof(StateHeader) + (size_t)env->p.n * E * 8 + 4 * E * 8 + E * 4 + tl * 8;
     if (h.has_word) b += tl * 4;
@@ -1307,6 +1316,17 @@ int sng_get_state(SngEnv *env, void *buf, size_t bytes, const double *episode_re
         out += n;
         return e;
     };
+    // the numpy streams live on the device: seeded here if no reference day drew from them yet
+    std::vector<uint32_t> np_words;
+    std::vector<int32_t> np_pos;
+    if (h.has_streams) {
+        int rc = ensure_np_streams(env, st);
+        if (rc) return rc;
+        np_words.resize(E * 2 * kMtN);
+        np_pos.resize(E);
+        HIP_TRY(env, hipMemcpyAsync(np_words.data(), env->rs.mt, np_words.size() * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipMemcpyAsync(np_pos.data(), env->rs.pos, E * 4, hipMemcpyDeviceToHost, st));
+    }
     HIP_TRY(env, hipMemcpyAsync(&h.day_counter, env->ds.episode, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(env, pull(env->ds.soc, (size_t)env->p.n * E * 8));
     HIP_TRY(env, pull(env->ds.bess, E * 8));
@@ -1323,7 +1343,11 @@ int sng_get_state(SngEnv *env, void *buf, size_t bytes, const double *episode_re
     if (h.has_streams) {
         uint32_t *w = reinterpret_cast<uint32_t *>(out);
         for (size_t i = 0; i < E; ++i) {
-            env->np_rng[i].save(w + (2 * i) * MT19937::kStateWords);
+            // numpy's RandomState: the current block's 624 words and mti (sng_mt.h MT19937::save)
+            uint32_t *o = w + (2 * i) * MT19937::kStateWords;
+            const int cur = np_pos[i] >> 16, mti = np_pos[i] & 0xffff;
+            std::memcpy(o, np_words.data() + (i * 2 + cur) * kMtN, kMtN * 4);
+            o[kMtN] = (uint32_t)mti;
             env->py_rng[i].save(w + (2 * i + 1) * MT19937::kStateWords);
         }
     }
@@ -1360,17 +1384,29 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
         in += n;
         return e;
     };
-    // the restored streams, checked before anything is changed
-    std::vector<MT19937> np_rng, py_rng;
+    // the restored streams, checked before anything is changed: Python's into host streams, numpy's
+    // into block 0 of the device streams (position = mti)
+    std::vector<MT19937> py_rng;
+    std::vector<uint32_t> np_words;
+    std::vector<int32_t> np_pos;
     if (h.has_streams) {
         const size_t off = h.total_bytes - E * 2 * MT19937::kStateWords * 4;
         const uint32_t *w = reinterpret_cast<const uint32_t *>(static_cast<const char *>(buf) + off);
-        np_rng.resize(E);
         py_rng.resize(E);
-        for (size_t i = 0; i < E; ++i)
-            if (!np_rng[i].load(w + (2 * i) * MT19937::kStateWords) ||
-                !py_rng[i].load(w + (2 * i + 1) * MT19937::kStateWords))
+        np_words.resize(E * kMtN);
+        np_pos.resize(E);
+        for (size_t i = 0; i < E; ++i) {
+            const uint32_t *np = w + (2 * i) * MT19937::kStateWords;
+            if (np[kMtN] > (uint32_t)kMtN + 1 || !py_rng[i].load(w + (2 * i + 1) * MT19937::kStateWords))
                 return fail(env, SNG_ERR_INVALID_ARGUMENT, "corrupt RNG stream state");
+            std::memcpy(np_words.data() + i * kMtN, np, kMtN * 4);
+            // mti = N + 1 (never seeded) cannot come from a seeded RandomState
+            np_pos[i] = (int32_t)std::min<uint32_t>(np[kMtN], (uint32_t)kMtN);
+        }
+        if (!env->rs.mt) {
+            HIP_TRY(env, hipMalloc(&env->rs.mt, E * 2 * kMtN * sizeof(uint32_t)));
+            HIP_TRY(env, hipMalloc(&env->rs.pos, E * sizeof(int32_t)));
+        }
     }
     HIP_TRY(env, hipMemcpyAsync(env->ds.episode, &h.day_counter, sizeof(uint64_t), hipMemcpyHostToDevice, st));
     HIP_TRY(env, push(env->ds.soc, (size_t)env->p.n * E * 8));
@@ -1384,6 +1420,11 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
     if (h.has_req) HIP_TRY(env, push(env->ds.req, tl * 8));
     if (h.has_prof) HIP_TRY(env, push(env->ds.prof, 2 * (size_t)(env->p.T + 3) * E * 8));
     if (h.has_return) HIP_TRY(env, push(episode_return, E * 8));
+    if (h.has_streams) {
+        HIP_TRY(env, hipMemcpy2DAsync(env->rs.mt, 2 * kMtN * sizeof(uint32_t), np_words.data(), kMtN * sizeof(uint32_t),
+                                      kMtN * sizeof(uint32_t), E, hipMemcpyHostToDevice, st));
+        HIP_TRY(env, hipMemcpyAsync(env->rs.pos, np_pos.data(), E * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    }
     HIP_TRY(env, hipStreamSynchronize(st));
     env->seed = h.seed;
     env->p.seed = h.seed;
@@ -1397,7 +1438,7 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
     env->gen_mode = h.gen_mode;
     env->gen_loaded = h.gen_loaded != 0;
     env->replays = h.replays;
-    env->np_rng = std::move(np_rng);
+    env->np_seeded = h.has_streams != 0;
     env->py_rng = std::move(py_rng);
     return SNG_OK;
 }

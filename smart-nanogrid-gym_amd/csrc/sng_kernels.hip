@@ -1586,6 +1586,203 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
     return e;
 }
 
+// ---------------------------------------------------------------------------------
+// Reference-RNG days on the GPU (SngRngMode SNG_RNG_REFERENCE): numpy's MT19937 stream of each env
+// (np.random.seed(seed + global env), RandomState's state and draw semantics, sng_mt.h restates them
+// for the host) drives ChargingStation.generate_initial_vehicle_presence_per_charger
+// (charging_station.py:200-279) draw for draw, and the day is encoded into the word / f64 aux (/ req)
+// timeline exactly as the host encoder does it (sng_api.cpp encode_day).  Three kernels:
+//   mt_seed_kernel     init_genrand per env (once per seeding)
+//   mt_prepare_kernel  per env, one wavefront: the state one twist ahead into the other block (the
+//                      twist's three dependent ranges, 64 words at a time, in LDS)
+//   ref_day_kernel     per env, one thread: the day's draws and its timeline
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {   // twist term of words kk, kk + 1
+    const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
+    return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+}
+
+// B = twist(A), both 624 words (MT19937's in-place twist, its ranges computed out of place):
+// B[k] = A[k+M] ^ mix(A[k], A[k+1]) for k < N-M; B[k] = B[k+M-N] ^ mix(A[k], A[k+1]) up to N-2;
+// B[N-1] = B[M-1] ^ mix(A[N-1], B[0]).
+__device__ __forceinline__ void mt_twist_wave(const uint32_t *A, uint32_t *B, int lane) {
+    constexpr int NM = kMtN - kMtM;   // 227
+    for (int k = lane; k < NM; k += kWave) B[k] = A[k + kMtM] ^ mt_mix(A[k], A[k + 1]);
+    wave_lds_fence();
+    for (int k = NM + lane; k < 2 * NM; k += kWave) B[k] = B[k - NM] ^ mt_mix(A[k], A[k + 1]);
+    wave_lds_fence();
+    for (int k = 2 * NM + lane; k < kMtN - 1; k += kWave) B[k] = B[k - NM] ^ mt_mix(A[k], A[k + 1]);
+    wave_lds_fence();
+    if (lane == 0) B[kMtN - 1] = B[kMtM - 1] ^ mt_mix(A[kMtN - 1], B[0]);
+    wave_lds_fence();
+}
+
+// the same by one thread, in place of the stream's exhausted other block (a day that draws past two
+// blocks: not reachable by the generator's draw counts, kept for completeness)
+__device__ __noinline__ void mt_twist_lane(const uint32_t *A, uint32_t *B) {
+    constexpr int NM = kMtN - kMtM;
+    for (int k = 0; k < NM; ++k) B[k] = A[k + kMtM] ^ mt_mix(A[k], A[k + 1]);
+    for (int k = NM; k < kMtN - 1; ++k) B[k] = B[k - NM] ^ mt_mix(A[k], A[k + 1]);
+    B[kMtN - 1] = B[kMtM - 1] ^ mt_mix(A[kMtN - 1], B[0]);
+}
+
+// np.random.seed(s): init_genrand(s & 0xffffffff); mti = N, so the first draw twists
+__global__ __launch_bounds__(256) void mt_seed_kernel(RefStreams rs, uint64_t seed0, int64_t E) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    uint32_t *b = rs.mt + (size_t)e * 2 * kMtN;
+    uint32_t x = (uint32_t)(seed0 + (uint64_t)e);
+    b[0] = x;
+    for (int i = 1; i < kMtN; ++i) {
+        x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
+        b[i] = x;
+    }
+    rs.pos[e] = kMtN;   // block 0, mti = N
+}
+
+// Before a day: an exhausted current block (mti = N) is replaced by its twist, and the block after the
+// current one is put into the other slot, so the day has >= 624 draws without a twist of its own.
+__global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t E) {
+    __shared__ uint32_t lds[4][2][kMtN];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
+    const int64_t e = (int64_t)blockIdx.x * 4 + wave;
+    if (e >= E) return;   // wave-uniform
+    const int32_t pos = rs.pos[e];
+    int cur = pos >> 16, mti = pos & 0xffff;
+    uint32_t *blk = rs.mt + (size_t)e * 2 * kMtN;
+    uint32_t *A = lds[wave][0], *B = lds[wave][1];
+    for (int k = lane; k < kMtN; k += kWave) A[k] = blk[cur * kMtN + k];
+    wave_lds_fence();
+    if (mti >= kMtN) {
+        mt_twist_wave(A, B, lane);
+        uint32_t *x = A;
+        A = B;
+        B = x;
+        cur ^= 1;
+        mti -= kMtN;
+        for (int k = lane; k < kMtN; k += kWave) blk[cur * kMtN + k] = A[k];
+    }
+    mt_twist_wave(A, B, lane);
+    for (int k = lane; k < kMtN; k += kWave) blk[(cur ^ 1) * kMtN + k] = B[k];
+    if (lane == 0) rs.pos[e] = (cur << 16) | mti;
+}
+
+// One env's numpy stream inside ref_day_kernel: RandomState.random_sample / uniform / randint
+// (legacy, masked rejection) over the tempered words of the prepared blocks (sng_mt.h, host twin).
+struct MtLane {
+    uint32_t *blk;
+    int cur, mti;
+    bool ready;   // the other block holds the next state (set by mt_prepare_kernel)
+    __device__ __forceinline__ uint32_t next() {
+        if (mti >= kMtN) {
+            if (!ready) mt_twist_lane(blk + cur * kMtN, blk + (cur ^ 1) * kMtN);
+            cur ^= 1;
+            mti = 0;
+            ready = false;
+        }
+        return mt_temper(blk[cur * kMtN + mti++]);
+    }
+    __device__ __forceinline__ double random() {
+        const int32_t a = (int32_t)(next() >> 5), b = (int32_t)(next() >> 6);
+        return (a * 67108864.0 + b) / 9007199254740992.0;
+    }
+    __device__ __forceinline__ double uniform(double lo, double hi) { return lo + (hi - lo) * random(); }
+    __device__ __forceinline__ int randint(int low, int high) {   // exclusive high; one value: no draw
+        if (high - 1 - low == 0) return low;
+        uint32_t mask = (uint32_t)(high - 1 - low);
+        mask |= mask >> 1;
+        mask |= mask >> 2;
+        mask |= mask >> 4;
+        mask |= mask >> 8;
+        mask |= mask >> 16;
+        const uint32_t rng = (uint32_t)(high - 1 - low);
+        uint32_t v;
+        while ((v = (next() & mask)) > rng) {
+        }
+        return low + (int)v;
+    }
+};
+
+// The day of every env: generate_day + encode_day (sng_api.cpp) on one thread per env, charger by
+// charger; the lanes of a wavefront step (charger, t) together, so the timeline stores coalesce.
+__global__ __launch_bounds__(256) void ref_day_kernel(Params p, DeviceState s, RefStreams rs, int64_t E, int i4,
+                                                      int i10, int i1) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    const int32_t pos = rs.pos[e];
+    MtLane rng{rs.mt + (size_t)e * 2 * kMtN, pos >> 16, pos & 0xffff, true};
+    const int T = p.T, n = p.n;
+    const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;   // as generate_kernel
+    const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
+                              : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
+    const uint32_t el4 = (uint32_t)e * 4u, el8 = (uint32_t)e * 8u;
+    for (int c = 0; c < n; ++c) {
+        const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
+        bool present = false, prev_occ = false;
+        int dep = 0, prev_rem = 0;
+        uint32_t cur_cap = 0;
+        double cur_req = 0.0, prev_req = 0.0;
+        for (int t = 0; t < T; ++t) {
+            bool arrived = false;
+            double soc_arr = 0.0;
+            if (!present) {
+                const double r = rng.random();
+                if ((r - 0.1) > 0.5) {   // round(random.rand() - 0.1) == 1 (charging_station.py:214-215)
+                    present = arrived = true;
+                    soc_arr = rng.uniform(0.1, 0.9);                            // :257-259
+                    const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
+                    (void)rng.uniform(lo, 1.0);                                 // discarded draw, :219
+                    cur_cap = p.diff_caps ? (uint32_t)rng.randint(15, 120) : 40u;   // :267-269
+                    cur_req = p.req_enabled ? rng.uniform(lo, 1.0) : 1.0;       // :261-265
+                    const int high = min(t + i10, T + i1), low = t + i4;       // :271-279
+                    dep = (low >= high) ? low : rng.randint(low, high);
+                }
+            }
+            const bool occ = present && t < dep;
+            if (!occ) present = false;
+            // encode_day: STATIC unless the running SoC carries over (occupied at t-1, no arrival)
+            const bool running = !arrived && prev_occ;
+            const int rem = occ ? dep - t : 0;
+            const bool pen = (uint32_t)prev_rem - pen_lo <= pen_span;   // prev_rem = 0: empty at t-1
+            const size_t plane = (size_t)t * n * (size_t)E;
+            bst(s.word + plane, el4, pack_word(occ, !running, pen, occ ? cur_cap : 0u, (uint32_t)rem), r4);
+            bst(s.aux + plane, el8, (occ && !running) ? soc_arr : 0.0, r8);
+            // Requested_SOC[c, t-1]; slot 0 holds Requested_SOC[c, T-1] (written after the loop)
+            if (p.req_stream && t > 0) bst(s.req + plane, el8, prev_req, r8);
+            prev_occ = occ;
+            prev_rem = rem;
+            prev_req = occ ? cur_req : 0.0;
+        }
+        if (p.req_stream) bst(s.req, el8, prev_req, r8);
+    }
+    rs.pos[e] = (rng.cur << 16) | rng.mti;
+}
+
+hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream) {
+    hipLaunchKernelGGL(mt_seed_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, rs, seed0, E);
+    return hipGetLastError();
+}
+
+// One reference-RNG day of every env into the word / aux (/ req) planes; ratio, pen0 and the t = 0
+// observation are the caller's (the Python stream stays on the host).
+hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
+                          int i1, hipStream_t stream) {
+    hipLaunchKernelGGL(mt_prepare_kernel, dim3((unsigned)((E + 3) / 4)), dim3(256), 0, stream, rs, E);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ref_day_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, p, s, rs, E, i4,
+                       i10, i1);
+    return hipGetLastError();
+}
+
 __global__ void bump_day_kernel(DeviceState s) { *s.episode += 1; }
 
 hipError_t launch_bump_day(const DeviceState &s, hipStream_t stream) {

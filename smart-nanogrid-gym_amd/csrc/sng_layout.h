@@ -94,6 +94,19 @@ struct Params {
     uint64_t seed;            // handle seed: env e's seed is seed + env_offset + e
 };
 
+// The reference RNG's numpy stream of every env on the device (SngRngMode SNG_RNG_REFERENCE): the
+// MT19937 state of np.random.seed(seed + global env) as numpy's RandomState keeps it, in two blocks per
+// env, env-major ([E][2][624] u32: one env's words are contiguous, so a lane drawing from its own
+// stream reads consecutive words).  pos[e] = cur << 16 | mti: block `cur` holds the state whose
+// tempered words mti..623 are the stream's next draws; mt_prepare_kernel puts the state one twist
+// later into the other block before a day is drawn.  The Python `random` stream (two or three draws a
+// day) stays on the host (sng_mt.h).
+struct RefStreams {
+    uint32_t *mt;
+    int32_t *pos;
+};
+constexpr int kMtN = 624, kMtM = 397;
+
 struct DeviceState {
     double *soc, *bess, *bess0, *ratio, *pen0;
     uint32_t *word;
