@@ -408,8 +408,8 @@ __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t 
         const float pf = __fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
         const float pdt = __fmul_rn(pf, p.dt_f);
         pc = (double)pf;
-        // RCP: exact reciprocal-fma division with r = 1/c from the LDS table; wide stations
-        // (no table, see StepLds) divide directly -- both are the IEEE quotient
+        // RCP: exact reciprocal-fma division with r ~ 1/c (the LDS table, or recip_cap); otherwise
+        // the division itself -- all are the IEEE quotient
         change = RCP ? div_by_cap((double)pdt, cap, rcap) : (double)pdt / cap;
     }
     const double calc = prev + change;
@@ -977,9 +977,18 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
                 if (c >= cend) break;
                 // 1/cap from the LDS table here, not ahead with the actions: it needs charger j's
                 // record, and reading every record's up front waited for all of them
+                // (wide stations: recip_cap instead of the LDS table, exact all the same -- div_by_cap)
+#ifdef SNG_X_WIDEDIV
                 rc[j] = kRows ? s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu] : 0.0;
+#else
+                rc[j] = kRows ? s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu] : recip_cap((double)((w[j] >> W_CAP_SHIFT) & 0xffu));
+#endif
                 const double aux_j = PK ? (double)__uint_as_float(auxh[j]) : aux[j];
+#ifdef SNG_X_WIDEDIV
                 const ChargerResult r = charger_step<FAST, kRows>(p, w[j], aux_j, run[j], req[j], av[j], t, rc[j]);
+#else
+                const ChargerResult r = charger_step<FAST, true>(p, w[j], aux_j, run[j], req[j], av[j], t, rc[j]);
+#endif
                 bst<kNT>(socv, el8, r.soc, (uint32_t)c * (uint32_t)E * 8u);
                 if (DIAG) {   // 'Charger power values' and the SOC[c, t] the day record holds
                     if (info.charger_power) info.charger_power[(size_t)e * n + c] = r.pw;
