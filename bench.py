@@ -12,8 +12,11 @@ action Box, 20 % exact zeros), pre-generated on the device outside the timed reg
 
 Rank 0 prints one JSON line.  `roofline` describes the dominant kernel (the fused step):
 achieved = SURVEY.md 8(d)'s algorithmic bytes per env-step, B(N) = 40 N + 65 (465 B at N = 10),
-x the envs of one launch / the mean launch time from HIP start/stop events attached to every
-step-kernel dispatch (eager days right after the timed region, on the stream the kernel runs on).
+x the envs of one launch / the step kernel's mean duration inside the day graphs: the HIP-event device
+time of a timed day (on the graphs' stream) less the reset kernel, over the T step dispatches -- the
+start-to-start time rocprofv3 reports for a graph's kernels.  The reset kernel's time and the isolated
+dispatch time of the step kernel (`eager_launch_us`, `frac_eager`) come from HIP start/stop events
+attached to every dispatch of eager days right after the timed region, on the stream the kernels run on.
 `frac_rocprof` is the same bytes over the average duration of that kernel in the committed
 rocprofv3 --kernel-trace --stats summary (profiles/), when one exists for this kernel; `traffic` is
 the HBM bytes per launch from the committed PMC passes, null if absent.  `cpu_baseline` is the C
@@ -220,21 +223,33 @@ def main():
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()   # on the stream the graphs are launched on (torch's current stream)
     for _ in range(args.steps // D):
         day()
     if xch is not None:
         xch.finish()   # the last replay's gather is part of the timed work
+    ev1.record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    # per-kernel device time: HIP start/stop events attached to every step-kernel dispatch
-    # (hipExtLaunchKernel) over eager days of the same env/actions, right after the timed region
-    kernel_ms = venv.time_step_kernels(acts, days=args.timing_days)
-    timing_src = (f"HIP start/stop events on each step-kernel dispatch (hipExtLaunchKernel), "
-                  f"{args.timing_days} eager days after the timed region, same stream/env/actions")
+    # the step kernel's average duration as the graphs run it: the day's device time (HIP events
+    # around the timed replays, on the graphs' stream) less the reset kernel, over the T step dispatches.
+    # Inside a graph every dispatch starts when the previous one ends, so this is the start-to-start
+    # time rocprofv3 --kernel-trace reports for the graph's step kernels.  The reset's own time and the
+    # isolated per-dispatch step time come from HIP start/stop events attached to each dispatch
+    # (hipExtLaunchKernel) over eager days of the same env/actions, right after the timed region.
+    day_gpu_us = ev0.elapsed_time(ev1) * 1e3 / args.steps
+    kernel_ms, reset_ms = venv.time_step_kernels(acts, days=args.timing_days, with_resets=True)
+    reset_us = float(np.mean(reset_ms)) * 1e3
+    graph_step_us = (day_gpu_us - reset_us) / T
+    timing_src = (f"in-graph: (HIP-event device time per timed day {day_gpu_us:.2f} us - reset kernel "
+                  f"{reset_us:.2f} us) / {T} step dispatches; reset and eager_launch_us from HIP start/stop "
+                  f"events on each dispatch (hipExtLaunchKernel), {args.timing_days} eager days after the "
+                  f"timed region, same stream/env/actions")
     elapsed = max_over_ranks(elapsed, device=device)
     # sanity: a day's returns are finite and <= 0
     ret = venv.return_d.cpu().numpy()
@@ -247,7 +262,7 @@ def main():
     if rank == 0:
         env_steps = world * E * T * args.steps
         value = env_steps / elapsed
-        launch_s = float(np.mean(kernel_ms)) / 1e3
+        launch_s = graph_step_us * 1e-6
         bpl = survey_bytes(N) * E
         achieved = bpl / launch_s / 1e9
         rp_us, rp_file = rocprof_average_us(kernel, args.extended_day or noise)
@@ -256,6 +271,8 @@ def main():
                 "kernel": kernel, "bytes_model": f"SURVEY.md 8(d) B(N) = 40N+65 = {survey_bytes(N)} B per env-step",
                 "bytes_per_launch": bpl, "layout_bytes_per_launch": step_kernel_bytes(N, noise) * E,
                 "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src,
+                "eager_launch_us": round(float(np.mean(kernel_ms)) * 1e3, 3), "reset_us": round(reset_us, 3),
+                "frac_eager": round(bpl / (float(np.mean(kernel_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                 "rocprof_avg_us": rp_us, "rocprof_file": rp_file,
                 "frac_rocprof": None if rp_us is None else round(bpl / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
         headline = (N == 10 and T == 24 and not noise)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 7
+#define SNG_ABI_VERSION 8
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -286,9 +286,11 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
 int sng_graph_launch(SngGraph *graph, void *stream);
 /* Kernel-time probe: runs `days` device-RNG days eagerly (as the graph does) and returns the
  * device time (ms) of every step kernel, ms[days*T], from HIP start/stop events attached to
- * each dispatch (hipExtLaunchKernel: the dispatch's own begin/end timestamps).  Synchronises. */
+ * each dispatch (hipExtLaunchKernel: the dispatch's own begin/end timestamps), and, when reset_ms
+ * is not NULL, of every day's device reset, reset_ms[days] (the one-launch generator the same way;
+ * wide stations' generator + profile + observe0 launches between recorded events).  Synchronises. */
 int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
-                          const SngInfo *info, int32_t days, float *ms, void *stream);
+                          const SngInfo *info, int32_t days, float *ms, float *reset_ms, void *stream);
 void sng_graph_destroy(SngGraph *graph);
 
 /* Host-only entry points (no GPU needed): the reference-RNG scenario generator, for

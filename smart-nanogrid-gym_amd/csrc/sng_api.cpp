@@ -33,7 +33,7 @@ hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, do
                            int vec_io, hipStream_t stream, int mode, int64_t replay);
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            float *obs, double *ep_return, int vec_io,
-                           hipStream_t stream);
+                           hipStream_t stream, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream);
 hipError_t launch_bump_day(const DeviceState &s, hipStream_t stream);
 hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream);
@@ -1113,9 +1113,21 @@ int sng_get_vehicle_soc(SngEnv *env, double *h, void *stream) {
     // [N][E] on the device -> [E][N] on the host
     std::vector<double> tmp((size_t)N * env->E);
     HIP_TRY(env, hipMemcpyAsync(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+    // a packed day: an empty charger's running SoC carries the next arrival's (sng_layout.h); SOC[c, t]
+    // shows 0 there.  Occupancy of the last stepped step t - 1 is its record's OCC bit (plane t)
+    std::vector<uint32_t> rec;
+    const bool packed_mid = env->p.packed && env->t >= 1;
+    if (packed_mid) {
+        rec.resize((size_t)N * env->E);
+        HIP_TRY(env, hipMemcpyAsync(rec.data(), reinterpret_cast<const uint32_t *>(env->ds.aux) + (size_t)env->t * rec.size(),
+                                    rec.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    }
     HIP_TRY(env, hipStreamSynchronize(st));
     for (int64_t e = 0; e < env->E; ++e)
-        for (int c = 0; c < N; ++c) h[e * N + c] = tmp[(size_t)c * env->E + e];
+        for (int c = 0; c < N; ++c) {
+            const size_t i = (size_t)c * env->E + e;
+            h[e * N + c] = (packed_mid && !(rec[i] & W_OCC)) ? 0.0 : tmp[i];
+        }
     return SNG_OK;
 }
 
@@ -1125,9 +1137,22 @@ int sng_set_vehicle_soc(SngEnv *env, const double *h, void *stream) {
     HIP_TRY(env, hipSetDevice(env->device));
     const int N = env->p.n;
     std::vector<double> tmp((size_t)N * env->E);
-    for (int64_t e = 0; e < env->E; ++e)
-        for (int c = 0; c < N; ++c) tmp[(size_t)c * env->E + e] = h[e * N + c];
     hipStream_t st = as_stream(stream);
+    // a packed day mid-day: empty chargers keep the arrival SoC their running SoC carries (sng_layout.h)
+    std::vector<uint32_t> rec;
+    const bool packed_mid = env->p.packed && env->t >= 1;
+    if (packed_mid) {
+        rec.resize(tmp.size());
+        HIP_TRY(env, hipMemcpyAsync(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipMemcpyAsync(rec.data(), reinterpret_cast<const uint32_t *>(env->ds.aux) + (size_t)env->t * rec.size(),
+                                    rec.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipStreamSynchronize(st));
+    }
+    for (int64_t e = 0; e < env->E; ++e)
+        for (int c = 0; c < N; ++c) {
+            const size_t i = (size_t)c * env->E + e;
+            if (!packed_mid || (rec[i] & W_OCC)) tmp[i] = h[e * N + c];
+        }
     HIP_TRY(env, hipMemcpyAsync(env->ds.soc, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipStreamSynchronize(st));
     return SNG_OK;
@@ -1153,12 +1178,12 @@ int sng_get_scenario(SngEnv *env, int64_t first, int64_t count, int32_t V, doubl
     const size_t rows = (size_t)T * N, pitch = (size_t)env->E, cnt = (size_t)count;
     std::vector<uint32_t> w(rows * cnt);
     std::vector<double> aux(rows * cnt), rq;
-    std::vector<uint64_t> rec;
-    if (env->p.packed) {   // device-RNG day: packed records in the aux buffer (sng_layout.h)
-        rec.resize(rows * cnt);
-        HIP_TRY(env, hipMemcpy2DAsync(rec.data(), cnt * sizeof(uint64_t),
-                                      reinterpret_cast<const uint64_t *>(env->ds.aux) + first, pitch * sizeof(uint64_t),
-                                      cnt * sizeof(uint64_t), rows, hipMemcpyDeviceToHost, st));
+    std::vector<uint32_t> rec;
+    if (env->p.packed) {   // device-RNG day: packed records in the aux buffer (sng_layout.h), T + 1 planes
+        rec.resize(rows * cnt + (size_t)N * cnt);
+        HIP_TRY(env, hipMemcpy2DAsync(rec.data(), cnt * sizeof(uint32_t),
+                                      reinterpret_cast<const uint32_t *>(env->ds.aux) + first, pitch * sizeof(uint32_t),
+                                      cnt * sizeof(uint32_t), rows + N, hipMemcpyDeviceToHost, st));
     } else {
         HIP_TRY(env, hipMemcpy2DAsync(w.data(), cnt * sizeof(uint32_t), env->ds.word + first, pitch * sizeof(uint32_t),
                                       cnt * sizeof(uint32_t), rows, hipMemcpyDeviceToHost, st));
@@ -1174,12 +1199,12 @@ int sng_get_scenario(SngEnv *env, int64_t first, int64_t count, int32_t V, doubl
     HIP_TRY(env, hipMemcpyAsync(pv_ratio, env->ds.ratio + first, cnt * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(env, hipStreamSynchronize(st));
     if (env->p.packed) {
-        for (size_t i = 0; i < rec.size(); ++i) {
-            w[i] = (uint32_t)rec[i];
-            const uint32_t hi = (uint32_t)(rec[i] >> 32);
-            float f;
-            std::memcpy(&f, &hi, sizeof f);
-            aux[i] = (double)f;
+        // step t's record is plane t + 1; an arrival's SoC is carried by the record before it (plane t),
+        // and an empty charger shows 0
+        const size_t plane = (size_t)N * cnt;
+        for (size_t i = 0; i < rows * cnt; ++i) {
+            w[i] = rec[plane + i];
+            aux[i] = (w[i] & W_STATIC) ? (double)rec_soc(rec[i]) : 0.0;
         }
     }
     for (size_t k = 0; k < cnt; ++k) {
@@ -1240,7 +1265,8 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 // ---------------------------------------------------------------------------------
 // Checkpoint / resume: header, then the sections in this order (host byte order):
 //   soc f64[N][E] | bess, bess0, ratio, pen0 f64[E] | flags u32[E] | [word u32[T][N][E], host days]
-//   | aux 8B[T][N][E] | [req f64[T][N][E]] | [prof f64[2][T+3][E]] | [episode return f64[E]]
+//   | aux 8B[T][N][E] (a packed day: its u32[T+1][N][E] records, sng_layout.h) | [req f64[T][N][E]]
+//   | [prof f64[2][T+3][E]] | [episode return f64[E]]
 //   | [reference streams u32[E][2][625]]
 // ---------------------------------------------------------------------------------
 struct StateHeader {
@@ -1537,7 +1563,7 @@ void sng_graph_destroy(SngGraph *g) {
 }
 
 int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
-                          const SngInfo *info, int32_t days, float *ms, void *stream) {
+                          const SngInfo *info, int32_t days, float *ms, float *reset_ms, void *stream) {
     if (!env || !actions || !obs || !reward || !done || !ms || days < 1)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     if (!device_rng_ok(env)) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
@@ -1556,13 +1582,16 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     const int64_t E = env->E;
     const int T = p.T, A = p.act_dim;
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
-    std::vector<hipEvent_t> ev(2 * (size_t)T * days, nullptr);
+    std::vector<hipEvent_t> ev(2 * (size_t)T * days, nullptr), rev(reset_ms ? 2 * (size_t)days : 0, nullptr);
     hipError_t e = hipSuccess;
     if (env->p.packed && env->p.bump_day && env->t == 0) e = launch_bump_day(env->ds, st);   // as in sng_reset
     for (auto &x : ev)
         if (e == hipSuccess) e = hipEventCreate(&x);
+    for (auto &x : rev)
+        if (e == hipSuccess) e = hipEventCreate(&x);
     for (int d = 0; e == hipSuccess && d < days; ++d) {
-        e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, obs, ip.episode_return, vec, st);
+        e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, obs, ip.episode_return, vec, st,
+                            reset_ms ? rev[2 * (size_t)d] : nullptr, reset_ms ? rev[2 * (size_t)d + 1] : nullptr);
         for (int t = 0; e == hipSuccess && t < T; ++t) {
             hipEvent_t a = ev[2 * ((size_t)d * T + t)], b = ev[2 * ((size_t)d * T + t) + 1];
             e = launch_step(p, env->ds, ip, env->host_tab, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, st, a, b);
@@ -1570,7 +1599,11 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     for (int k = 0; e == hipSuccess && k < T * days; ++k) e = hipEventElapsedTime(&ms[k], ev[2 * k], ev[2 * k + 1]);
+    for (int d = 0; e == hipSuccess && reset_ms && d < days; ++d)
+        e = hipEventElapsedTime(&reset_ms[d], rev[2 * (size_t)d], rev[2 * (size_t)d + 1]);
     for (auto x : ev)
+        if (x) (void)hipEventDestroy(x);
+    for (auto x : rev)
         if (x) (void)hipEventDestroy(x);
     if (e != hipSuccess) return hip_fail(env, e, "timed day");
     env->p.req_stream = p.req_stream;

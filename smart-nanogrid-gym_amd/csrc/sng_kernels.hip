@@ -661,15 +661,14 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
     const double bess_l = bld(p.bess ? s.bess : s.ratio, el8);   // stream re-reads ratio
     const double pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
     const double ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
-    uint32_t w[NC], auxh[NC];
+    uint32_t w[NC];
     double aux[NC], run[NC], req[NC];
+    const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
         const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
-        if (PK) {   // packed device-day record: word | float32 aux << 32 (sng_layout.h)
-            const uint64_t rec = bld(reinterpret_cast<const uint64_t *>(s.aux + plane), el8, r8);
-            w[c] = (uint32_t)rec;
-            auxh[c] = (uint32_t)(rec >> 32);
+        if (PK) {   // packed device-day record (sng_layout.h): plane t + 1
+            w[c] = bld(rec_t, el4, r4);
         } else {
             w[c] = bld(s.word + plane, el4, r4);
             aux[c] = bld(s.aux + plane, el8, r8);
@@ -703,12 +702,14 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             const uint32_t capi = (w[c] >> W_CAP_SHIFT) & 0xffu;
-            const double aux_c = PK ? (double)__uint_as_float(auxh[c]) : aux[c];
-            const ChargerResult r =
-                charger_step<true, true>(p, w[c], aux_c, run[c], req[c], av[c], t, recip_cap((double)capi));
-            bst<kNT>(s.soc, el8, r.soc, (uint32_t)c * (uint32_t)E * 8u);
+            // a packed day: an arriving vehicle's SoC is the running SoC the step before stored (the
+            // record it carried), so the step sees no STATIC bit and an empty charger's SoC is 0
+            const bool occ = (w[c] & W_OCC) != 0;
+            const ChargerResult r = charger_step<true, true>(p, PK ? (w[c] & ~W_STATIC) : w[c], PK ? 0.0 : aux[c], run[c],
+                                                             req[c], av[c], t, recip_cap((double)capi));
+            bst<kNT>(s.soc, el8, (PK && !occ) ? (double)rec_soc(w[c]) : r.soc, (uint32_t)c * (uint32_t)E * 8u);
             o_row[k_soc + c] = (float)r.soc;
-            o_row[k_soc + NC + c] = departure_obs(w[c]);
+            o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[c]);
             n_nonexist += r.nx;
             fl |= r.fl;
             pen_v += r.q;
@@ -828,8 +829,10 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;   // byte offsets of the env
     const uint32_t *__restrict__ word_t = word + tbase * (size_t)E;   // this step's timeline planes
     const double *__restrict__ aux_t = auxv + tbase * (size_t)E;
+    // a packed day's records: plane t + 1 (sng_layout.h)
+    const uint32_t *__restrict__ rec_t = reinterpret_cast<const uint32_t *>(auxv) + (tbase + n) * (size_t)E;
     const double *__restrict__ req_t = reqv + tbase * (size_t)E;
-    uint32_t w[CH], auxh[CH];
+    uint32_t w[CH];
     double aux[CH], run[CH], req[CH];
     auto load_state = [&](int c0) {
 #pragma unroll
@@ -837,10 +840,8 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             const int c = c0 + j;
             if (c < cend) {
                 const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
-                if (PK) {   // packed device-day record: word | float32 aux << 32 (sng_layout.h)
-                    const uint64_t rec = bld(reinterpret_cast<const uint64_t *>(aux_t), el8, r8);
-                    w[j] = (uint32_t)rec;
-                    auxh[j] = (uint32_t)(rec >> 32);   // widened where charger j is computed
+                if (PK) {   // packed device-day record (sng_layout.h)
+                    w[j] = bld(rec_t, el4, r4);
                 } else {
                     w[j] = bld(word_t, el4, r4);
                     aux[j] = bld(aux_t, el8, r8);
@@ -849,7 +850,6 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
             } else {
                 w[j] = 0u;
                 aux[j] = run[j] = 0.0;
-                auxh[j] = 0u;
             }
         }
     };
@@ -983,19 +983,22 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
 #else
                 rc[j] = kRows ? s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu] : recip_cap((double)((w[j] >> W_CAP_SHIFT) & 0xffu));
 #endif
-                const double aux_j = PK ? (double)__uint_as_float(auxh[j]) : aux[j];
+                // a packed day: the arrival SoC is the running SoC the step before stored (sng_layout.h)
+                const bool occ = (w[j] & W_OCC) != 0;
+                const uint32_t wj = PK ? (w[j] & ~W_STATIC) : w[j];
+                const double aux_j = PK ? 0.0 : aux[j];
 #ifdef SNG_X_WIDEDIV
-                const ChargerResult r = charger_step<FAST, kRows>(p, w[j], aux_j, run[j], req[j], av[j], t, rc[j]);
+                const ChargerResult r = charger_step<FAST, kRows>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
 #else
-                const ChargerResult r = charger_step<FAST, true>(p, w[j], aux_j, run[j], req[j], av[j], t, rc[j]);
+                const ChargerResult r = charger_step<FAST, true>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
 #endif
-                bst<kNT>(socv, el8, r.soc, (uint32_t)c * (uint32_t)E * 8u);
+                bst<kNT>(socv, el8, (PK && !occ) ? (double)rec_soc(w[j]) : r.soc, (uint32_t)c * (uint32_t)E * 8u);
                 if (DIAG) {   // 'Charger power values' and the SOC[c, t] the day record holds
                     if (info.charger_power) info.charger_power[(size_t)e * n + c] = r.pw;
                     if (info.vehicle_soc) info.vehicle_soc[(size_t)e * n + c] = r.soc;
                 }
                 o_row[k_soc + c] = (float)r.soc;
-                o_row[k_soc + n + c] = departure_obs(w[j]);
+                o_row[k_soc + n + c] = departure_obs((PK && !occ) ? 0u : w[j]);
                 n_nonexist += r.nx;
                 fl |= r.fl;
                 if (L == 1) {
@@ -1164,10 +1167,12 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 const int c = c0 + j < n ? c0 + j : n - 1;
-                if (PK) {   // packed device-day record (sng_layout.h)
-                    const uint64_t rec = reinterpret_cast<const uint64_t *>(auxv)[(size_t)c * E + e];
-                    w[j] = (uint32_t)rec;
-                    aux[j] = (double)__uint_as_float((uint32_t)(rec >> 32));
+                if (PK) {   // packed device-day records (sng_layout.h): t = 0 is plane 1; plane 0 carries
+                            // the SoC of the t = 0 arrivals
+                    const uint32_t *rec = reinterpret_cast<const uint32_t *>(auxv);
+                    const uint32_t r = rec[((size_t)n + c) * E + e];
+                    w[j] = (r & W_OCC) ? r : 0u;   // an empty charger's record carries a SoC, not a departure
+                    aux[j] = (r & W_OCC) ? (double)rec_soc(rec[(size_t)c * E + e]) : 0.0;
                 } else {
                     w[j] = word[(size_t)c * E + e];
                     aux[j] = auxv[(size_t)c * E + e];
@@ -1228,7 +1233,7 @@ constexpr int kDayVehicles = 8;
 constexpr float kInvLog2Q = -1.3569154488567239f;   // 1 / log2(0.6)
 
 __host__ __device__ constexpr size_t generate_lds_bytes(bool with_req) {
-    return (size_t)kDayVehicles * kGenBlock * (sizeof(uint32_t) + sizeof(double) + (with_req ? sizeof(double) : 0));
+    return (size_t)kDayVehicles * kGenBlock * (sizeof(uint32_t) + sizeof(float) + (with_req ? sizeof(double) : 0));
 }
 
 // One vehicle's draws (charging_station.py:257-279), in stream order: the geometric wait from
@@ -1324,19 +1329,26 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 // Grid (E / 256, N + 1): blocks y < N write charger y's timeline, blocks y = N the t = 0
 // observation (observe_day0).  The day counter is read here and advanced by the day's first step
 // (step_kernel, t = 0), so no block of this grid waits on another.
+#ifdef SNG_GEN_NT
+constexpr int kGenRecPol = kNT;   // A/B variant: the timeline records as streaming stores
+#else
+constexpr int kGenRecPol = 0;
+#endif
 __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
                                                              int i4, int i10, int i1, float *__restrict__ obs,
                                                              double *__restrict__ ep_return, int vec_io) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     uint32_t *s_veh = reinterpret_cast<uint32_t *>(lds);                        // [V][BLOCK] arr | dep<<8 | cap<<16
-    double *s_soc = reinterpret_cast<double *>(s_veh + kDayVehicles * kGenBlock);   // [V][BLOCK]
-    double *s_req = s_soc + kDayVehicles * kGenBlock;                             // [V][BLOCK] (req only)
+    float *s_soc = reinterpret_cast<float *>(s_veh + kDayVehicles * kGenBlock);   // [V][BLOCK] float32 draws
+    double *s_req = reinterpret_cast<double *>(s_soc + kDayVehicles * kGenBlock);   // [V][BLOCK] (req only)
     const int tid = threadIdx.x;
     const int64_t e = (int64_t)blockIdx.x * kGenBlock + tid;
     const int c = blockIdx.y;
     const uint64_t day = *s.episode;
     if (c == p.n) {
+#ifndef SNG_GX_NOOBS   // diagnostic builds (tools/gpu_session.sh ablib) only: generator cost breakdown
         observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds);
+#endif
         return;
     }
     if (e >= E) return;
@@ -1348,10 +1360,14 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     int tfree = 0, nv = 0;
     for (int v = 0; v < kDayVehicles - 1; ++v) {   // the last slot holds the sentinel
         if (tfree >= T) break;
+#ifdef SNG_GX_NOPH1
+        VehicleDraw d{tfree + 1, tfree + 7, 40u, 0.5, 0u};
+#else
         const VehicleDraw d = draw_vehicle(p, rng, tfree, i4, i10, i1);
+#endif
         if (d.ta >= T) break;
         s_veh[v * kGenBlock + tid] = (uint32_t)d.ta | ((uint32_t)d.dep << 8) | (d.cap << 16);
-        s_soc[v * kGenBlock + tid] = d.soc;
+        s_soc[v * kGenBlock + tid] = (float)d.soc;   // a float32 value (draw_vehicle)
         if (p.req_enabled) {
             const double lo = d.soc <= 0.9 ? d.soc + 0.1 : 1.0;
             s_req[v * kGenBlock + tid] = lo + (1.0 - lo) * u32_unit(d.req_draw);
@@ -1363,14 +1379,17 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     // slot nv: a sentinel that never arrives (arrival = departure = 255), so phase 2 walks the
     // list without a per-step bound check or branch (nv <= 7 < kDayVehicles, checked on the host)
     s_veh[nv * kGenBlock + tid] = 0xffffu;
-    s_soc[nv * kGenBlock + tid] = 0.0;
+    s_soc[nv * kGenBlock + tid] = 0.0f;
     if (p.req_enabled) s_req[nv * kGenBlock + tid] = 1.0;
 
-    // phase 2: the timeline
+    // phase 2: the timeline.  An empty step's record carries the SoC of a vehicle arriving at the
+    // next step (sng_layout.h), and plane 0 that of a vehicle arriving at t = 0.  cur = list[v] is the
+    // vehicle of step t (until it has departed), nxt = list[v + 1] the one after it, read from LDS a
+    // step before it can be needed; the record is assembled branch-free.
+    uint32_t cur = s_veh[tid], nxt = s_veh[kGenBlock + tid];
+    float soc_cur = s_soc[tid], soc_nxt = s_soc[kGenBlock + tid];
+    double req_cur = p.req_enabled ? s_req[tid] : 1.0, req_nxt = p.req_enabled ? s_req[kGenBlock + tid] : 1.0;
     int v = 0;
-    uint32_t cur = s_veh[tid];
-    double soc_cur = s_soc[tid];
-    double req_cur = p.req_enabled ? s_req[tid] : 1.0;
     bool prev_occ = false;
     int prev_rem = 0;
     // penalty-check list built by observe(t-1) (charging_station.py:42-63) as one unsigned range
@@ -1379,31 +1398,50 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
-    const uint32_t el8 = (uint32_t)e * 8u;
-    const uint32_t r8 = (uint32_t)c * (uint32_t)E * 8u;
+    const uint32_t el4 = (uint32_t)e * 4u, el8 = (uint32_t)e * 8u;
+    const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
+    uint32_t *rec = reinterpret_cast<uint32_t *>(s.aux);
+    const size_t nE = (size_t)n * (size_t)E;
+    // raw buffer stores: the plane in the V#, the charger row in soffset, the env in the lane offset
+    bst<kGenRecPol>(rec, el4, ((cur & 0xffu) == 0u) ? rec_carry(false, soc_cur) : 0u, r4);
     for (int t = 0; t < T; ++t) {
-        v += (t > (int)((cur >> 8) & 0xffu)) ? 1 : 0;   // past the current departure: next vehicle
-        cur = s_veh[v * kGenBlock + tid];                // (re-)read unconditionally: no divergence
-        soc_cur = s_soc[v * kGenBlock + tid];
-        if (p.req_enabled) req_cur = s_req[v * kGenBlock + tid];
+        // the vehicle of step t + 1: past the current departure, the next one (the list ends in a
+        // sentinel that never arrives or departs)
+        const bool adv = t + 1 > (int)((cur >> 8) & 0xffu);
+        const uint32_t v1 = adv ? nxt : cur;
+        const float soc1 = adv ? soc_nxt : soc_cur;
+        const double req1 = adv ? req_nxt : req_cur;
+        v += adv ? 1 : 0;
+        const int vr = v + 1 < kDayVehicles ? v + 1 : kDayVehicles - 1;   // list[v + 1] for step t + 1
+        const uint32_t nxt1 = s_veh[vr * kGenBlock + tid];
+        const float soc_nxt1 = s_soc[vr * kGenBlock + tid];
+        const double req_nxt1 = p.req_enabled ? s_req[vr * kGenBlock + tid] : 1.0;
+
         const int ta = (int)(cur & 0xffu), dep = (int)((cur >> 8) & 0xffu);
         const uint32_t cap = (cur >> 16) & 0xffu;
         const bool occ = t >= ta && t < dep;
         const bool arrived = t == ta;
         const bool pen = (uint32_t)prev_rem - pen_lo <= pen_span;   // prev_rem = 0: charger empty at t-1
         const int rem = occ ? dep - t : 0;
-        // raw buffer stores: the step's plane in the V#, the charger row in soffset, the env in
-        // the 32-bit lane offset
-        const size_t plane = (size_t)t * n * (size_t)E;
-        // packed record (sng_layout.h): word | float32 bits of the aux value << 32, dense
-        const uint32_t word = pack_word(occ, arrived, pen, occ ? cap : 0u, (uint32_t)rem);
-        const uint64_t rec = (uint64_t)word | ((uint64_t)__float_as_uint(arrived ? (float)soc_cur : 0.0f) << 32);
-        bst(reinterpret_cast<uint64_t *>(s.aux) + plane, el8, rec, r8);
+        const uint32_t w_occ = pack_word(true, arrived, pen, cap, (uint32_t)rem);
+        const uint32_t carry = ((int)(v1 & 0xffu) == t + 1) ? rec_carry(false, soc1) : 0u;
+        const uint32_t w_emp = (pen ? W_PEN : 0u) | carry;
+        const uint32_t m = 0u - (uint32_t)occ;
+#ifdef SNG_GX_NOPH2
+        if (((w_occ & m) | (w_emp & ~m)) == 0xdeadbeefu)
+#endif
+        bst<kGenRecPol>(rec + (size_t)(t + 1) * nE, el4, (w_occ & m) | (w_emp & ~m), r4);
         // requested SoC timeline (sng_layout.h): Requested_SOC[c, t-1] at t >= 1 -- the step reads
         // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
-        if (p.req_stream && t > 0) bst(s.req + plane, el8, prev_occ ? req_cur : 0.0, r8);
+        if (p.req_stream && t > 0) bst(s.req + (size_t)t * nE, el8, prev_occ ? req_cur : 0.0, r8);
         prev_occ = occ;
         prev_rem = rem;
+        cur = v1;
+        soc_cur = soc1;
+        req_cur = req1;
+        nxt = nxt1;
+        soc_nxt = soc_nxt1;
+        req_nxt = req_nxt1;
     }
     if (p.req_stream) bst(s.req, el8, prev_occ ? req_cur : 0.0, r8);
 }
@@ -1581,17 +1619,26 @@ hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hip
 // a few generator workgroups per CU still fit); wider stations keep profile_kernel and
 // observe0_kernel as separate launches behind the generator.
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
-                           float *obs, double *ep_return, int vec_io, hipStream_t stream) {
+                           float *obs, double *ep_return, int vec_io, hipStream_t stream, hipEvent_t ev_start,
+                           hipEvent_t ev_stop) {
     const size_t veh = generate_lds_bytes(p.req_enabled != 0), tile = (size_t)round4(kGenBlock * p.obs_dim) * 4;
     const bool fused = tile <= 48 * 1024;
     const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(p.n + (fused ? 1 : 0))), block(kGenBlock);
-    hipLaunchKernelGGL(generate_kernel, grid, block, (fused && tile > veh) ? tile : veh, stream, p, s, seed, E, i4, i10,
-                       i1, obs, ep_return, vec_io);
-    if (fused) return hipGetLastError();
+    const size_t lds = (fused && tile > veh) ? tile : veh;
+    if (fused && ev_start && ev_stop) {   // the one-launch reset, timed by its own dispatch timestamps
+        hipExtLaunchKernelGGL(generate_kernel, grid, block, lds, stream, ev_start, ev_stop, 0u, p, s, seed, E, i4, i10,
+                              i1, obs, ep_return, vec_io);
+        return hipGetLastError();
+    }
+    if (ev_start) (void)hipEventRecord(ev_start, stream);
+    hipLaunchKernelGGL(generate_kernel, grid, block, lds, stream, p, s, seed, E, i4, i10, i1, obs, ep_return, vec_io);
     hipError_t e = hipGetLastError();
-    if (e == hipSuccess) e = launch_profiles(p, s, E, stream);
-    // the PV ratio and pen0 of the day, from the streams, as the fused t = 0 blocks do
-    if (e == hipSuccess) e = launch_observe0(p, s, obs, ep_return, E, vec_io, stream, OBS0_DEVICE, -1);
+    if (!fused) {
+        if (e == hipSuccess) e = launch_profiles(p, s, E, stream);
+        // the PV ratio and pen0 of the day, from the streams, as the fused t = 0 blocks do
+        if (e == hipSuccess) e = launch_observe0(p, s, obs, ep_return, E, vec_io, stream, OBS0_DEVICE, -1);
+    }
+    if (e == hipSuccess && ev_stop) e = hipEventRecord(ev_stop, stream);
     return e;
 }
 

@@ -12,10 +12,18 @@
 //   aux    f64 [T][N][E]    per charger-step static SoC: the "previous" SoC when the word's
 //                           STATIC bit is set (arrival: SOC[c, t] as generated), else the
 //                           SOC[c, t] an unoccupied charger shows
-//   rec    u64 [T][N][E]    device-RNG days only, in the aux buffer (`word` unused): the packed
-//                           record word | float32 bits of the aux value << 32 -- one 8 B load or
-//                           store per charger-step instead of 12 B in two; the device generator
-//                           draws its arrival SoC as a float32 value, so the record is exact
+//   rec    u32 [T+1][N][E]  device-RNG days only, in the aux buffer (`word` unused): one 4 B record
+//                           per charger-step instead of 12 B in two planes.  Plane t + 1 is step t's
+//                           record; plane 0 is a record "before the day".  An occupied charger's
+//                           record is its word (bits below).  An empty charger's record keeps OCC = 0
+//                           and PEN, and carries the arrival SoC of the vehicle that arrives at the
+//                           next step (REC_SOC, below; 0 when none): every arrival at t >= 1 follows an
+//                           empty step (the departure step stays empty, charging_station.py:239-251),
+//                           and plane 0 carries the t = 0 arrivals.  The step kernel stores the
+//                           carried SoC as an empty charger's running SoC, so the arrival step reads
+//                           it as the previous SoC; an empty charger shows 0 in the observation.  The
+//                           device generator draws its arrival SoC as a float32 value in [0.1, 0.9],
+//                           so the 25-bit field holds it exactly
 //   req    f64 [T][N][E]    Requested_SOC[c, t-1] (read by the penalty check where W_PEN is set);
 //                           the t = 0 slot, never read by a step, holds Requested_SOC[c, T-1] so the
 //                           day can be exported (sng_get_scenario); only when enabled
@@ -29,6 +37,10 @@
 //                      (charging_station.py:42-63); evaluated at step t
 //   bits 8-15  CAP     vehicle capacity in kWh used at step t (integer, 15..119 or 40)
 //   bits 16-23 DEP     departure time - t of the vehicle present at t (observation), 0 if none
+//
+// Packed record of an empty charger (OCC = 0): bit 2 PEN as above, bits 3-27 REC_SOC = the float32
+// bits of the next step's arrival SoC less 123 << 23 (a float in [2^-4, 1) has a biased exponent in
+// 123..126: 2 exponent bits + 23 mantissa bits), 0 when no vehicle arrives at the next step.
 #pragma once
 #include <stdint.h>
 
@@ -55,6 +67,16 @@ SNG_HD inline uint32_t pack_word(bool occ, bool stat, bool pen, uint32_t cap, ui
     return (occ ? W_OCC : 0u) | (stat ? W_STATIC : 0u) | (pen ? W_PEN : 0u) | ((cap & 0xffu) << W_CAP_SHIFT) |
            ((dep & 0xffu) << W_DEP_SHIFT);
 }
+
+constexpr int REC_SOC_SHIFT = 3;
+constexpr uint32_t kRecSocBias = 123u << 23;
+
+// An empty charger's packed record carrying arrival SoC `soc` (a float32 value in [2^-4, 1)).
+SNG_HD inline uint32_t rec_carry(bool pen, float soc) {
+    return (pen ? W_PEN : 0u) | ((__builtin_bit_cast(uint32_t, soc) - kRecSocBias) << REC_SOC_SHIFT);
+}
+// The arrival SoC an empty charger's record carries (meaningful when the next step is an arrival).
+SNG_HD inline float rec_soc(uint32_t rec) { return __builtin_bit_cast(float, (rec >> REC_SOC_SHIFT) + kRecSocBias); }
 
 // Constant tables, in device memory, read with scalar (wave-uniform) loads.
 struct Tables {

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SNG_LIBRARY", os.path.join(os.path.dirname(PKG_DIR), 
 DATA_DIR = os.path.join(PKG_DIR, "data")
 IRRADIANCE_FILE = os.path.join(DATA_DIR, "solar_irradiance_1min.f64")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 SNG_OK = 0
 RNG_REFERENCE = 0
 RNG_DEVICE = 1
@@ -134,7 +134,7 @@ EXPORTS = {
     "sng_graph_destroy": (None, [ctypes.c_void_p]),
     "sng_time_step_kernels": (ctypes.c_int, [_H, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.POINTER(SngInfo), ctypes.c_int32, c_float_p,
-                                             _S]),
+                                             c_float_p, _S]),
     "sng_host_generate_scenarios": (ctypes.c_int, [ctypes.POINTER(SngConfig), ctypes.c_int64, ctypes.c_uint64,
                                                    ctypes.c_int32, c_double_p, c_double_p, c_double_p, c_double_p,
                                                    c_int32_p, c_int32_p, ctypes.c_int32, c_double_p]),

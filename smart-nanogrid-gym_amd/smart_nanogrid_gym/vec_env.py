@@ -519,18 +519,21 @@ class SmartNanogridVecEnv:
         ivs, ratio = self.get_scenarios(int(env_index), 1, max_vehicles)
         return ivs[0], float(ratio[0])
 
-    def time_step_kernels(self, actions, days=1):
+    def time_step_kernels(self, actions, days=1, with_resets=False):
         """Device time (ms) of every step kernel over `days` eager device-RNG days, from HIP
-        start/stop events attached to each kernel dispatch; actions [T, E, act_dim] on the device."""
+        start/stop events attached to each kernel dispatch; actions [T, E, act_dim] on the device.
+        with_resets: also return every day's reset time (ms), as (steps, resets)."""
         a = actions.contiguous()
         out = np.zeros(days * self.timesteps, np.float32)
+        res = np.zeros(days, np.float32) if with_resets else None
         with torch.cuda.device(self.device):
             check(lib().sng_time_step_kernels(self._h, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(self.obs_d.data_ptr()),
                                               ctypes.c_void_p(self.reward_d.data_ptr()),
                                               ctypes.c_void_p(self.done_d.data_ptr()), ctypes.byref(self._info),
                                               days, out.ctypes.data_as(_native.c_float_p),
+                                              None if res is None else res.ctypes.data_as(_native.c_float_p),
                                               _stream_handle(self.device)), self._h)
-        return out
+        return (out, res) if with_resets else out
 
     def tables(self):
         n = ctypes.c_int32()
