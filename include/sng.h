@@ -288,7 +288,8 @@ int sng_graph_launch(SngGraph *graph, void *stream);
  * device time (ms) of every step kernel, ms[days*T], from HIP start/stop events attached to
  * each dispatch (hipExtLaunchKernel: the dispatch's own begin/end timestamps), and, when reset_ms
  * is not NULL, of every day's device reset, reset_ms[days] (the one-launch generator the same way;
- * wide stations' generator + profile + observe0 launches between recorded events).  Synchronises. */
+ * wide stations' generator + profile + observe0 launches between recorded events).  ms = NULL: the
+ * days are launched without per-dispatch events (back to back, for a caller's own timing).  Synchronises. */
 int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
                           const SngInfo *info, int32_t days, float *ms, float *reset_ms, void *stream);
 void sng_graph_destroy(SngGraph *graph);

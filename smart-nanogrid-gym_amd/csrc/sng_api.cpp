@@ -1564,7 +1564,7 @@ void sng_graph_destroy(SngGraph *g) {
 
 int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
                           const SngInfo *info, int32_t days, float *ms, float *reset_ms, void *stream) {
-    if (!env || !actions || !obs || !reward || !done || !ms || days < 1)
+    if (!env || !actions || !obs || !reward || !done || days < 1)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     if (!device_rng_ok(env)) return fail(env, SNG_ERR_UNSUPPORTED, "device RNG needs time_interval <= 2h");
     HIP_TRY(env, hipSetDevice(env->device));
@@ -1582,7 +1582,7 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     const int64_t E = env->E;
     const int T = p.T, A = p.act_dim;
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
-    std::vector<hipEvent_t> ev(2 * (size_t)T * days, nullptr), rev(reset_ms ? 2 * (size_t)days : 0, nullptr);
+    std::vector<hipEvent_t> ev(ms ? 2 * (size_t)T * days : 0, nullptr), rev(reset_ms ? 2 * (size_t)days : 0, nullptr);
     hipError_t e = hipSuccess;
     if (env->p.packed && env->p.bump_day && env->t == 0) e = launch_bump_day(env->ds, st);   // as in sng_reset
     for (auto &x : ev)
@@ -1593,12 +1593,12 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
         e = launch_generate(p, env->ds, env->seed, E, env->i4, env->i10, env->i1, obs, ip.episode_return, vec, st,
                             reset_ms ? rev[2 * (size_t)d] : nullptr, reset_ms ? rev[2 * (size_t)d + 1] : nullptr);
         for (int t = 0; e == hipSuccess && t < T; ++t) {
-            hipEvent_t a = ev[2 * ((size_t)d * T + t)], b = ev[2 * ((size_t)d * T + t) + 1];
+            hipEvent_t a = ms ? ev[2 * ((size_t)d * T + t)] : nullptr, b = ms ? ev[2 * ((size_t)d * T + t) + 1] : nullptr;
             e = launch_step(p, env->ds, ip, env->host_tab, actions + (size_t)t * E * A, obs, reward, done, E, t, vec, st, a, b);
         }
     }
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    for (int k = 0; e == hipSuccess && k < T * days; ++k) e = hipEventElapsedTime(&ms[k], ev[2 * k], ev[2 * k + 1]);
+    for (int k = 0; e == hipSuccess && ms && k < T * days; ++k) e = hipEventElapsedTime(&ms[k], ev[2 * k], ev[2 * k + 1]);
     for (int d = 0; e == hipSuccess && reset_ms && d < days; ++d)
         e = hipEventElapsedTime(&reset_ms[d], rev[2 * (size_t)d], rev[2 * (size_t)d + 1]);
     for (auto x : ev)

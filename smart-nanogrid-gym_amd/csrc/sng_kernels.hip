@@ -1329,11 +1329,11 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 // Grid (E / 256, N + 1): blocks y < N write charger y's timeline, blocks y = N the t = 0
 // observation (observe_day0).  The day counter is read here and advanced by the day's first step
 // (step_kernel, t = 0), so no block of this grid waits on another.
-#ifdef SNG_GEN_NT
-constexpr int kGenRecPol = kNT;   // A/B variant: the timeline records as streaming stores
-#else
-constexpr int kGenRecPol = 0;
-#endif
+// The timeline records leave as streaming (nontemporal) stores: reset 24.5-24.7 -> 22.5-22.7 us per day
+// at 65,536 x 10 (A/B, one box), the steps' code and state staying in L2.  Diagnostic builds
+// (tools/gpu_session.sh ablib) split the reset's time: without the t = 0 observation blocks 24.3-24.9 us
+// (they run beside the timeline blocks), without phase 1's draws 20.7, without the record stores 16-16.8.
+constexpr int kGenRecPol = kNT;
 __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
                                                              int i4, int i10, int i1, float *__restrict__ obs,
                                                              double *__restrict__ ep_return, int vec_io) {

@@ -519,6 +519,16 @@ class SmartNanogridVecEnv:
         ivs, ratio = self.get_scenarios(int(env_index), 1, max_vehicles)
         return ivs[0], float(ratio[0])
 
+    def run_eager_days(self, actions, days=1):
+        """`days` device-RNG days (reset + T steps each) launched eagerly from C, back to back, without
+        per-dispatch events (sng_time_step_kernels with ms = NULL); synchronises."""
+        a = actions.contiguous()
+        with torch.cuda.device(self.device):
+            check(lib().sng_time_step_kernels(self._h, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(self.obs_d.data_ptr()),
+                                              ctypes.c_void_p(self.reward_d.data_ptr()),
+                                              ctypes.c_void_p(self.done_d.data_ptr()), ctypes.byref(self._info),
+                                              days, None, None, _stream_handle(self.device)), self._h)
+
     def time_step_kernels(self, actions, days=1, with_resets=False):
         """Device time (ms) of every step kernel over `days` eager device-RNG days, from HIP
         start/stop events attached to each kernel dispatch; actions [T, E, act_dim] on the device.
