@@ -52,11 +52,11 @@ def survey_bytes(n):
 
 def step_kernel_bytes(n, noise=False):
     """What this layout moves per env-step of a device-RNG day (b-pv, no requested-SoC stream): actions
-    4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N + packed charger-step record 8N (scenario
-    word + float32 static SoC) + BESS r/w 16 + PV ratio 8 + day-return r/w 16 = 36N + 89 (+ 64 for the
-    PV / price profile factors of t..t+3 with stochastic profiles).  Host-RNG days read the word and a
-    float64 static SoC instead: 40N + 89."""
-    return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 8 * n + 16 + 8 + 16 + (64 if noise else 0)
+    4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N + packed 4-byte charger-step record 4N
+    (sng_layout.h) + BESS r/w 16 + PV ratio 8 + day-return r/w 16 = 32N + 89 (+ 64 for the PV / price
+    profile factors of t..t+3 with stochastic profiles).  Host-RNG days read the word and a float64
+    static SoC instead: 40N + 89."""
+    return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 4 * n + 16 + 8 + 16 + (64 if noise else 0)
 
 
 def _cpu_worker(job):
