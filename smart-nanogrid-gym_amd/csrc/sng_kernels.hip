@@ -779,8 +779,12 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
 // Every per-charger load of a lane's batch is issued before any of it is used, and the first
 // batch before the action staging wait, so one lane keeps 3*CH + 2 requests in flight.
 // ---------------------------------------------------------------------------------
+// One wavefront per SIMD at the bench's population (1,024 waves), so the kernel may use the whole register
+// file: amdgpu_waves_per_eu(1, 1) lets the wide stations' prefetched batch live in registers (at the
+// default two waves per SIMD the compiler spilled it to scratch).
 template <int NC, int L, bool DIAG, bool FAST, bool PK>
-__global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceState s, InfoPtrs info,
+__global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(1, 1))) void step_kernel(
+    Params p, DeviceState s, InfoPtrs info,
                                                               const float *__restrict__ act, float *__restrict__ obs,
                                                               double *__restrict__ reward, uint8_t *__restrict__ done,
                                                               int64_t E, int t, int vec_io) {
@@ -872,6 +876,36 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
         load_req(c0);
         load_state(c0);
     };
+    // Wide single-lane stations (several batches): batch b + 1's loads are issued before batch b is
+    // computed, so they land while it computes instead of after it (the loop is not unrolled: the
+    // prefetched registers are copied into the batch's at the top of the next iteration).
+    constexpr bool kPF = (L == 1) && !kRows && (NC > 0) && (CH < NC) && (NC % CH == 0)
+#ifdef SNG_WIDE_NOPF
+                         && false   // A/B build: batches loaded in turn
+#endif
+        ;
+    constexpr int PFN = kPF ? CH : 1;
+    uint32_t wn[PFN];
+    double auxn[PFN], runn[PFN], reqn[PFN];
+    auto load_next = [&](int c0) {
+        if constexpr (kPF) {
+            const bool rq_live = p.req_stream && !p.req_zero;
+            const double rq = p.req_zero ? 0.0 : 1.0;
+#pragma unroll
+            for (int j = 0; j < CH; ++j) {
+                const int c = c0 + j;
+                const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
+                if (PK) {
+                    wn[j] = bld(rec_t, el4, r4);
+                } else {
+                    wn[j] = bld(word_t, el4, r4);
+                    auxn[j] = bld(aux_t, el8, r8);
+                }
+                runn[j] = bld(socv, el8, r8);
+                reqn[j] = rq_live ? bld(req_t, el8, r8) : rq;
+            }
+        }
+    };
 
     // 1. per-env values: pointer selects rather than branches (a disabled stream re-reads ratio)
     const double ratio = bld(s.ratio, el8);
@@ -961,7 +995,20 @@ __global__ __launch_bounds__(step_block(NC)) void step_kernel(Params p, DeviceSt
     uint32_t fl = 0;
     if (live) {
         for (int c0 = cbeg; c0 < cend; c0 += CH) {
-            if (c0 != cbeg) load_batch(c0);
+            if constexpr (kPF) {   // NC % CH == 0: every batch is full
+                if (c0 != cbeg) {
+#pragma unroll
+                    for (int j = 0; j < CH; ++j) {
+                        w[j] = wn[j];
+                        if (!PK) aux[j] = auxn[j];
+                        run[j] = runn[j];
+                        req[j] = reqn[j];
+                    }
+                }
+                if (c0 + CH < cend) load_next(c0 + CH);
+            } else if (c0 != cbeg) {
+                load_batch(c0);
+            }
             // the batch's actions ahead of the LDS writes below (they issue back to back)
             float av[CH];
             double rc[CH];
