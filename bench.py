@@ -18,7 +18,9 @@ start-to-start time rocprofv3 reports for a graph's kernels.  The reset kernel's
 dispatch time of the step kernel (`eager_launch_us`, `frac_eager`) come from HIP start/stop events
 attached to every dispatch of eager days right after the timed region, on the stream the kernels run on.
 `frac_rocprof` is the same bytes over the average duration of that kernel in the committed
-rocprofv3 --kernel-trace --stats summary (profiles/), when one exists for this kernel; `traffic` is
+rocprofv3 --kernel-trace --stats summary (profiles/), when one exists for this kernel;
+`measured_copy_gbs` is this GPU's device-to-device copy bandwidth (1 GiB, read + write bytes), the
+measured ceiling SURVEY.md 8(d) asks to quote beside the 8 TB/s spec; `traffic` is
 the HBM bytes per launch from the committed PMC passes, null if absent.  `cpu_baseline` is the C
 restatement of the reference's step()/reset() (oracle/, kind "port", label "restatement") run as one
 process per host core of sched_getaffinity (capped by OMP_NUM_THREADS), measured before the GPU is
@@ -134,11 +136,33 @@ def load_pmc_traffic(n_envs, chargers, kernel):
     return None
 
 
+def measured_copy_gbs(device, mib=1024, reps=5):
+    """Device-to-device copy bandwidth on this GPU (read + write bytes / time), the measured ceiling the
+    roofline is also quoted against: torch's copy kernel over two 1 GiB buffers, HIP events,
+    best of `reps`."""
+    n = mib * (1 << 20) // 4
+    a = torch.empty(n, dtype=torch.float32, device=device).fill_(1.0)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    best = None
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        best = ms if best is None else min(best, ms)
+    del a, b
+    torch.cuda.empty_cache()
+    return 2 * n * 4 / (best * 1e-3) / 1e9
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="timed simulated days")
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100, help="timed simulated days")
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--chargers", type=int, default=10)
     ap.add_argument("--time-interval", default="1h", help="'15min' with --extended-day = BASELINE config 5")
@@ -266,6 +290,7 @@ def main():
         bpl = survey_bytes(N) * E
         achieved = bpl / launch_s / 1e9
         rp_us, rp_file = rocprof_average_us(kernel, args.extended_day or noise)
+        copy_gbs = measured_copy_gbs(device)
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N, kernel),
                 "kernel": kernel, "bytes_model": f"SURVEY.md 8(d) B(N) = 40N+65 = {survey_bytes(N)} B per env-step",
@@ -273,6 +298,7 @@ def main():
                 "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src,
                 "eager_launch_us": round(float(np.mean(kernel_ms)) * 1e3, 3), "reset_us": round(reset_us, 3),
                 "frac_eager": round(bpl / (float(np.mean(kernel_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "measured_copy_gbs": round(copy_gbs, 1), "frac_of_measured_copy": round(achieved / copy_gbs, 4),
                 "rocprof_avg_us": rp_us, "rocprof_file": rp_file,
                 "frac_rocprof": None if rp_us is None else round(bpl / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
         headline = (N == 10 and T == 24 and not noise)
