@@ -339,6 +339,25 @@ int host_threads() {
     return std::max(1, std::min(n, 64));
 }
 
+// fn(begin, end) over [0, n) in contiguous ranges on host_threads() threads (the calling thread
+// takes the first range); serial below `grain` items per thread.
+template <class Fn>
+void parallel_ranges(int64_t n, int64_t grain, Fn &&fn) {
+    const int nt = (int)std::min<int64_t>(host_threads(), std::max<int64_t>(1, n / grain));
+    if (nt <= 1) {
+        fn((int64_t)0, n);
+        return;
+    }
+    const int64_t per = (n + nt - 1) / nt;
+    std::vector<std::thread> th;
+    for (int w = 1; w < nt; ++w) {
+        const int64_t b = w * per, en = std::min(n, b + per);
+        if (b < en) th.emplace_back([&fn, b, en] { fn(b, en); });
+    }
+    fn((int64_t)0, std::min(n, per));
+    for (auto &x : th) x.join();
+}
+
 // FNV-1a over a byte range (the checkpoint's configuration fingerprint)
 uint64_t fnv1a(const void *data, size_t n, uint64_t h = 1469598103934665603ull) {
     const unsigned char *b = static_cast<const unsigned char *>(data);
@@ -476,7 +495,23 @@ int ensure_staging(SngEnv *env, bool with_req) {
 void ensure_streams(SngEnv *env) {
     if (!env->py_rng.empty()) return;
     env->py_rng.resize(env->E);
-    for (int64_t i = 0; i < env->E; ++i) env->py_rng[i].seed_python(env->seed + (uint64_t)env->p.env_offset + (uint64_t)i);
+    const uint64_t s0 = env->seed + (uint64_t)env->p.env_offset;
+    parallel_ranges(env->E, 1024, [env, s0](int64_t b, int64_t en) {
+        for (int64_t i = b; i < en; ++i) env->py_rng[i].seed_python(s0 + (uint64_t)i);
+    });
+}
+
+// random_pv_shift_ratio = random.randint(0, 180) / 100 from every env's Python stream
+// (smart_nanogrid_environment.py:349), after the day-end draw the last step still owes (:181),
+// into the pinned h_ratio; the streams are independent, so host threads take ranges of envs.
+void draw_ratios(SngEnv *env) {
+    const bool end_draw = env->day_finished;
+    parallel_ranges(env->E, 4096, [env, end_draw](int64_t b, int64_t en) {
+        for (int64_t i = b; i < en; ++i) {
+            if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
+            env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;
+        }
+    });
 }
 
 // ... and numpy's on the device (mt_seed_kernel), queued on `st`.
@@ -942,11 +977,7 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     if (rc) return rc;
     env->p.req_stream = with_req ? 1 : 0;
     HIP_TRY(env, launch_ref_day(env->p, env->ds, env->rs, env->E, env->i4, env->i10, env->i1, st));
-    const bool end_draw = env->day_finished;
-    for (int64_t i = 0; i < env->E; ++i) {
-        if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
-        env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;
-    }
+    draw_ratios(env);
     std::fill(env->h_pen0, env->h_pen0 + env->E, 0.0);   // python index -1 of a generated day holds zeros
     rc = finish_host_day(env, with_req, obs, st);
     if (rc) return rc;
@@ -972,11 +1003,7 @@ int sng_reset_replay(SngEnv *env, float *obs, void *stream) {
         ensure_streams(env);
         int rc = ensure_staging(env, false);
         if (rc) return rc;
-        const bool end_draw = env->day_finished;
-        for (int64_t i = 0; i < env->E; ++i) {
-            if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
-            env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;
-        }
+        draw_ratios(env);
         HIP_TRY(env, hipMemcpyAsync(env->ds.ratio, env->h_ratio, env->E * sizeof(double), hipMemcpyHostToDevice, st));
         HIP_TRY(env, hipEventRecord(env->staging_done, st));
         env->p.req_zero = 1;

@@ -1381,13 +1381,21 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 // (tools/gpu_session.sh ablib) split the reset's time: without the t = 0 observation blocks 24.3-24.9 us
 // (they run beside the timeline blocks), without phase 1's draws 20.7, without the record stores 16-16.8.
 constexpr int kGenRecPol = kNT;
+// Vehicle list entries (LDS) are kept in the record's own layout: arrival step in bits 0-7 (the flag
+// bits of a record, masked off), capacity in 8-15 and departure step in 16-23, so an occupied step's
+// record is (entry & 0xffff00 | flags) - t << 16 (the departure field becomes the steps left; it is
+// > t while the vehicle is present, so nothing borrows); the arrival SoC is kept as the carry bits an
+// empty record holds (rec_carry), computed once per vehicle in phase 1.  TT: the day's step count as
+// a compile-time constant (the walk unrolled: 24 for the 1 h day), 0 for a runtime p.T; REQ: the
+// requested-SoC stream.
+template <int TT, bool REQ>
 __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
                                                              int i4, int i10, int i1, float *__restrict__ obs,
                                                              double *__restrict__ ep_return, int vec_io) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    uint32_t *s_veh = reinterpret_cast<uint32_t *>(lds);                        // [V][BLOCK] arr | dep<<8 | cap<<16
-    float *s_soc = reinterpret_cast<float *>(s_veh + kDayVehicles * kGenBlock);   // [V][BLOCK] float32 draws
-    double *s_req = reinterpret_cast<double *>(s_soc + kDayVehicles * kGenBlock);   // [V][BLOCK] (req only)
+    uint32_t *s_veh = reinterpret_cast<uint32_t *>(lds);                      // [V][BLOCK] arr | cap<<8 | dep<<16
+    uint32_t *s_car = s_veh + kDayVehicles * kGenBlock;                        // [V][BLOCK] arrival SoC carry bits
+    double *s_req = reinterpret_cast<double *>(s_car + kDayVehicles * kGenBlock);   // [V][BLOCK] (REQ only)
     const int tid = threadIdx.x;
     const int64_t e = (int64_t)blockIdx.x * kGenBlock + tid;
     const int c = blockIdx.y;
@@ -1401,7 +1409,8 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     if (e >= E) return;
     const uint64_t ge = (uint64_t)(e + p.env_offset);   // global env id
     HashStream rng{stream_key(seed, ge, (uint32_t)c, day), 0u};
-    const int T = p.T, n = p.n;
+    const int T = TT > 0 ? TT : p.T;
+    const int n = p.n;
 
     // phase 1 (charging_station.py:200-279)
     int tfree = 0, nv = 0;
@@ -1413,9 +1422,9 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const VehicleDraw d = draw_vehicle(p, rng, tfree, i4, i10, i1);
 #endif
         if (d.ta >= T) break;
-        s_veh[v * kGenBlock + tid] = (uint32_t)d.ta | ((uint32_t)d.dep << 8) | (d.cap << 16);
-        s_soc[v * kGenBlock + tid] = (float)d.soc;   // a float32 value (draw_vehicle)
-        if (p.req_enabled) {
+        s_veh[v * kGenBlock + tid] = (uint32_t)d.ta | (d.cap << W_CAP_SHIFT) | ((uint32_t)d.dep << W_DEP_SHIFT);
+        s_car[v * kGenBlock + tid] = rec_carry(false, (float)d.soc);   // a float32 value (draw_vehicle)
+        if (REQ) {
             const double lo = d.soc <= 0.9 ? d.soc + 0.1 : 1.0;
             s_req[v * kGenBlock + tid] = lo + (1.0 - lo) * u32_unit(d.req_draw);
         }
@@ -1423,22 +1432,22 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         tfree = d.dep + 1;   // the departure step stays empty (charging_station.py:239-251)
     }
 
-    // slot nv: a sentinel that never arrives (arrival = departure = 255), so phase 2 walks the
-    // list without a per-step bound check or branch (nv <= 7 < kDayVehicles, checked on the host)
-    s_veh[nv * kGenBlock + tid] = 0xffffu;
-    s_soc[nv * kGenBlock + tid] = 0.0f;
-    if (p.req_enabled) s_req[nv * kGenBlock + tid] = 1.0;
+    // slot nv: a sentinel that never arrives or departs (arrival = departure = 255), so phase 2 walks
+    // the list without a per-step bound check or branch (nv <= 7 < kDayVehicles, checked on the host)
+    s_veh[nv * kGenBlock + tid] = 0xffu | (0xffu << W_DEP_SHIFT);
+    s_car[nv * kGenBlock + tid] = 0u;
+    if (REQ) s_req[nv * kGenBlock + tid] = 1.0;
 
     // phase 2: the timeline.  An empty step's record carries the SoC of a vehicle arriving at the
     // next step (sng_layout.h), and plane 0 that of a vehicle arriving at t = 0.  cur = list[v] is the
     // vehicle of step t (until it has departed), nxt = list[v + 1] the one after it, read from LDS a
     // step before it can be needed; the record is assembled branch-free.
     uint32_t cur = s_veh[tid], nxt = s_veh[kGenBlock + tid];
-    float soc_cur = s_soc[tid], soc_nxt = s_soc[kGenBlock + tid];
-    double req_cur = p.req_enabled ? s_req[tid] : 1.0, req_nxt = p.req_enabled ? s_req[kGenBlock + tid] : 1.0;
+    uint32_t car_cur = s_car[tid], car_nxt = s_car[kGenBlock + tid];
+    double req_cur = REQ ? s_req[tid] : 1.0, req_nxt = REQ ? s_req[kGenBlock + tid] : 1.0;
     int v = 0;
     bool prev_occ = false;
-    int prev_rem = 0;
+    uint32_t prev_rem = 0u;
     // penalty-check list built by observe(t-1) (charging_station.py:42-63) as one unsigned range
     // test on the steps the vehicle at t-1 had left: on_departure {1}, sparse {1..3}, dense any;
     // no_penalty never (lo = 256 > any remainder)
@@ -1450,47 +1459,45 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     uint32_t *rec = reinterpret_cast<uint32_t *>(s.aux);
     const size_t nE = (size_t)n * (size_t)E;
     // raw buffer stores: the plane in the V#, the charger row in soffset, the env in the lane offset
-    bst<kGenRecPol>(rec, el4, ((cur & 0xffu) == 0u) ? rec_carry(false, soc_cur) : 0u, r4);
+    bst<kGenRecPol>(rec, el4, ((cur & 0xffu) == 0u) ? car_cur : 0u, r4);
+#pragma unroll
     for (int t = 0; t < T; ++t) {
         // the vehicle of step t + 1: past the current departure, the next one (the list ends in a
         // sentinel that never arrives or departs)
-        const bool adv = t + 1 > (int)((cur >> 8) & 0xffu);
+        const bool adv = (uint32_t)(t + 1) > (cur >> W_DEP_SHIFT);
         const uint32_t v1 = adv ? nxt : cur;
-        const float soc1 = adv ? soc_nxt : soc_cur;
+        const uint32_t car1 = adv ? car_nxt : car_cur;
         const double req1 = adv ? req_nxt : req_cur;
         v += adv ? 1 : 0;
         const int vr = v + 1 < kDayVehicles ? v + 1 : kDayVehicles - 1;   // list[v + 1] for step t + 1
         const uint32_t nxt1 = s_veh[vr * kGenBlock + tid];
-        const float soc_nxt1 = s_soc[vr * kGenBlock + tid];
-        const double req_nxt1 = p.req_enabled ? s_req[vr * kGenBlock + tid] : 1.0;
+        const uint32_t car_nxt1 = s_car[vr * kGenBlock + tid];
+        const double req_nxt1 = REQ ? s_req[vr * kGenBlock + tid] : 1.0;
 
-        const int ta = (int)(cur & 0xffu), dep = (int)((cur >> 8) & 0xffu);
-        const uint32_t cap = (cur >> 16) & 0xffu;
-        const bool occ = t >= ta && t < dep;
-        const bool arrived = t == ta;
-        const bool pen = (uint32_t)prev_rem - pen_lo <= pen_span;   // prev_rem = 0: charger empty at t-1
-        const int rem = occ ? dep - t : 0;
-        const uint32_t w_occ = pack_word(true, arrived, pen, cap, (uint32_t)rem);
-        const uint32_t carry = ((int)(v1 & 0xffu) == t + 1) ? rec_carry(false, soc1) : 0u;
+        const uint32_t ta = cur & 0xffu, dep = cur >> W_DEP_SHIFT;
+        const bool occ = (uint32_t)t >= ta && (uint32_t)t < dep;
+        const bool pen = prev_rem - pen_lo <= pen_span;   // prev_rem = 0: charger empty at t-1
+        const uint32_t flags = W_OCC | ((uint32_t)t == ta ? W_STATIC : 0u) | (pen ? W_PEN : 0u);
+        const uint32_t w_occ = ((cur & 0xffff00u) | flags) - ((uint32_t)t << W_DEP_SHIFT);   // dep -> dep - t
+        const uint32_t carry = ((v1 & 0xffu) == (uint32_t)(t + 1)) ? car1 : 0u;
         const uint32_t w_emp = (pen ? W_PEN : 0u) | carry;
-        const uint32_t m = 0u - (uint32_t)occ;
 #ifdef SNG_GX_NOPH2
-        if (((w_occ & m) | (w_emp & ~m)) == 0xdeadbeefu)
+        if ((occ ? w_occ : w_emp) == 0xdeadbeefu)
 #endif
-        bst<kGenRecPol>(rec + (size_t)(t + 1) * nE, el4, (w_occ & m) | (w_emp & ~m), r4);
+        bst<kGenRecPol>(rec + (size_t)(t + 1) * nE, el4, occ ? w_occ : w_emp, r4);
         // requested SoC timeline (sng_layout.h): Requested_SOC[c, t-1] at t >= 1 -- the step reads
         // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
-        if (p.req_stream && t > 0) bst(s.req + (size_t)t * nE, el8, prev_occ ? req_cur : 0.0, r8);
+        if (REQ && t > 0) bst(s.req + (size_t)t * nE, el8, prev_occ ? req_cur : 0.0, r8);
         prev_occ = occ;
-        prev_rem = rem;
+        prev_rem = occ ? dep - (uint32_t)t : 0u;
         cur = v1;
-        soc_cur = soc1;
+        car_cur = car1;
         req_cur = req1;
         nxt = nxt1;
-        soc_nxt = soc_nxt1;
+        car_nxt = car_nxt1;
         req_nxt = req_nxt1;
     }
-    if (p.req_stream) bst(s.req, el8, prev_occ ? req_cur : 0.0, r8);
+    if (REQ) bst(s.req, el8, prev_occ ? req_cur : 0.0, r8);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1672,13 +1679,16 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
     const bool fused = tile <= 48 * 1024;
     const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(p.n + (fused ? 1 : 0))), block(kGenBlock);
     const size_t lds = (fused && tile > veh) ? tile : veh;
+    const bool req = p.req_enabled != 0;
+    auto kern = p.T == 24 ? (req ? generate_kernel<24, true> : generate_kernel<24, false>)
+                          : (req ? generate_kernel<0, true> : generate_kernel<0, false>);
     if (fused && ev_start && ev_stop) {   // the one-launch reset, timed by its own dispatch timestamps
-        hipExtLaunchKernelGGL(generate_kernel, grid, block, lds, stream, ev_start, ev_stop, 0u, p, s, seed, E, i4, i10,
-                              i1, obs, ep_return, vec_io);
+        hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev_start, ev_stop, 0u, p, s, seed, E, i4, i10, i1, obs,
+                              ep_return, vec_io);
         return hipGetLastError();
     }
     if (ev_start) (void)hipEventRecord(ev_start, stream);
-    hipLaunchKernelGGL(generate_kernel, grid, block, lds, stream, p, s, seed, E, i4, i10, i1, obs, ep_return, vec_io);
+    hipLaunchKernelGGL(kern, grid, block, lds, stream, p, s, seed, E, i4, i10, i1, obs, ep_return, vec_io);
     hipError_t e = hipGetLastError();
     if (!fused) {
         if (e == hipSuccess) e = launch_profiles(p, s, E, stream);
