@@ -507,7 +507,11 @@ void ensure_streams(SngEnv *env) {
 void draw_ratios(SngEnv *env) {
     const bool end_draw = env->day_finished;
     parallel_ranges(env->E, 4096, [env, end_draw](int64_t b, int64_t en) {
+        // the streams are 2.5 KB apart: two prefetch stages (the position word 16 streams ahead, the
+        // next state word 8 ahead) keep the misses of many streams in flight
         for (int64_t i = b; i < en; ++i) {
+            if (i + 16 < en) __builtin_prefetch(env->py_rng[i + 16].pos_addr());
+            if (i + 8 < en) __builtin_prefetch(env->py_rng[i + 8].next_addr());
             if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
             env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;
         }
@@ -1398,7 +1402,7 @@ int sng_get_state(SngEnv *env, void *buf, size_t bytes, const double *episode_re
         for (size_t i = 0; i < E; ++i) {
             // numpy's RandomState: the current block's 624 words and mti (sng_mt.h MT19937::save)
             uint32_t *o = w + (2 * i) * MT19937::kStateWords;
-            const int cur = np_pos[i] >> 16, mti = np_pos[i] & 0xffff;
+            const int cur = (np_pos[i] >> 16) & 1, mti = np_pos[i] & kMtPosMask;
             std::memcpy(o, np_words.data() + (i * 2 + cur) * kMtN, kMtN * 4);
             o[kMtN] = (uint32_t)mti;
             env->py_rng[i].save(w + (2 * i + 1) * MT19937::kStateWords);

@@ -1761,17 +1761,25 @@ __global__ __launch_bounds__(256) void mt_seed_kernel(RefStreams rs, uint64_t se
     rs.pos[e] = kMtN;   // block 0, mti = N
 }
 
-// Before a day: an exhausted current block (mti = N) is replaced by its twist, and the block after the
-// current one is put into the other slot, so the day has >= 624 draws without a twist of its own.
+// Before a day: an exhausted current block (mti = N) is replaced by its successor, and the block after the
+// current one is put into the other slot, so the day has >= 624 draws without a twist of its own.  The
+// position word is cur << 16 | kMtNextReady | mti; kMtNextReady says the other slot already holds the
+// current block's successor (a day of ~300 draws leaves it untouched), so most days need no twist here.
 __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t E) {
     __shared__ uint32_t lds[4][2][kMtN];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const int64_t e = (int64_t)blockIdx.x * 4 + wave;
     if (e >= E) return;   // wave-uniform
     const int32_t pos = rs.pos[e];
-    int cur = pos >> 16, mti = pos & 0xffff;
+    int cur = (pos >> 16) & 1, mti = pos & kMtPosMask;
+    const bool next_ready = (pos & kMtNextReady) != 0;
+    if (next_ready && mti < kMtN) return;   // nothing to prepare
     uint32_t *blk = rs.mt + (size_t)e * 2 * kMtN;
     uint32_t *A = lds[wave][0], *B = lds[wave][1];
+    if (mti >= kMtN && next_ready) {   // the successor is in place: it becomes the current block
+        cur ^= 1;
+        mti -= kMtN;
+    }
     for (int k = lane; k < kMtN; k += kWave) A[k] = blk[cur * kMtN + k];
     wave_lds_fence();
     if (mti >= kMtN) {
@@ -1785,7 +1793,7 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
     }
     mt_twist_wave(A, B, lane);
     for (int k = lane; k < kMtN; k += kWave) blk[(cur ^ 1) * kMtN + k] = B[k];
-    if (lane == 0) rs.pos[e] = (cur << 16) | mti;
+    if (lane == 0) rs.pos[e] = (cur << 16) | kMtNextReady | mti;
 }
 
 // One env's numpy stream inside ref_day_kernel: RandomState.random_sample / uniform / randint
@@ -1831,7 +1839,7 @@ __global__ __launch_bounds__(256) void ref_day_kernel(Params p, DeviceState s, R
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= E) return;
     const int32_t pos = rs.pos[e];
-    MtLane rng{rs.mt + (size_t)e * 2 * kMtN, pos >> 16, pos & 0xffff, true};
+    MtLane rng{rs.mt + (size_t)e * 2 * kMtN, (pos >> 16) & 1, pos & kMtPosMask, true};
     const int T = p.T, n = p.n;
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;   // as generate_kernel
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
@@ -1876,7 +1884,7 @@ __global__ __launch_bounds__(256) void ref_day_kernel(Params p, DeviceState s, R
         }
         if (p.req_stream) bst(s.req, el8, prev_req, r8);
     }
-    rs.pos[e] = (rng.cur << 16) | rng.mti;
+    rs.pos[e] = (rng.cur << 16) | (rng.ready ? kMtNextReady : 0) | rng.mti;   // no block switch: the successor stays
 }
 
 hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream) {

@@ -128,6 +128,8 @@ struct RefStreams {
     int32_t *pos;
 };
 constexpr int kMtN = 624, kMtM = 397;
+// RefStreams::pos word: cur << 16 | kMtNextReady | mti (mti <= 624)
+constexpr int32_t kMtNextReady = 0x4000, kMtPosMask = 0x3fff;
 
 struct DeviceState {
     double *soc, *bess, *bess0, *ratio, *pen0;

@@ -80,6 +80,9 @@ class MT19937 {
     }
 
     // checkpoint / resume (sng_get_state): the 624 state words and the position
+    // prefetch targets of the next draw (the host ratio draws walk tens of thousands of streams)
+    const void *pos_addr() const { return &mti_; }
+    const void *next_addr() const { return &mt_[mti_ < N ? mti_ : 0]; }
     static constexpr int kStateWords = N + 1;
     void save(uint32_t *out) const {
         for (int i = 0; i < N; ++i) out[i] = mt_[i];

@@ -24,14 +24,16 @@ from smart_nanogrid_gym import SmartNanogridVecEnv  # noqa: E402
 from smart_nanogrid_gym._native import lib  # noqa: E402
 
 
-def timed(fn, repeats):
+def timed(fn, repeats, sync=True):
     out = []
     for _ in range(repeats):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         fn()
-        torch.cuda.synchronize()
+        if sync:
+            torch.cuda.synchronize()
         out.append((time.perf_counter() - t0) * 1e3)
+    torch.cuda.synchronize()
     return {"median_ms": float(np.median(out)), "min_ms": float(np.min(out)), "max_ms": float(np.max(out))}
 
 
@@ -55,6 +57,12 @@ def main():
         for t in range(v.timesteps):
             v.step_tensors(zero)
         res["replay_reset"] = timed(lambda: v.replay_tensors(), args.repeats)
+        # the host part alone: the call returns once its work is queued (no stream sync)
+        res["replay_call_only"] = timed(lambda: v.replay_tensors(), args.repeats, sync=False)
+        res["reference_call_only"] = timed(lambda: v.reset_tensors(rng="reference"), args.repeats, sync=False)
+        os.environ["SNG_HOST_THREADS"] = "1"
+        res["replay_reset_1thread"] = timed(lambda: v.replay_tensors(), args.repeats)
+        del os.environ["SNG_HOST_THREADS"]
         res["timeline_mb"] = round(v.timesteps * args.chargers * E * 12 / 1e6, 1)
         print(json.dumps(res), flush=True)
         v.close()
