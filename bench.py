@@ -2,7 +2,7 @@
 
 Metric (BASELINE.json): env-steps/sec (whole node) at 65,536 envs x 10 chargers, 24-step day.
 One bench "step" = one simulated day for every env on every GPU: GPU-RNG reset (new
-vehicles) + 24 fused step kernels, replayed as hipGraphs of 4 days.  When N > 1 every day's
+vehicles) + 24 fused step kernels, replayed as hipGraphs of 20 days.  When N > 1 every day's
 per-env returns are all-gathered over RCCL, one collective per replay on the collective
 stream, overlapped with the next replay's kernels.  Actions are synthetic (uniform in the
 action Box, 20 % exact zeros), pre-generated on the device outside the timed region.
@@ -174,7 +174,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing-days", type=int, default=3, help="eager days for the per-kernel HIP-event probe")
-    ap.add_argument("--graph-days", type=int, default=4, help="days per graph replay (divides steps)")
+    ap.add_argument("--graph-days", type=int, default=20, help="days per graph replay (divides steps)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

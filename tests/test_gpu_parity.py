@@ -136,6 +136,34 @@ def test_batched_reference_rng_vs_oracle_bit_exact(E, N, mode, lanes):
     venv.close()
 
 
+@pytest.mark.parametrize("E,N,days", [(64, 10, 12), (32, 50, 6), (16, 128, 3)])
+def test_reference_rng_many_days_stream_blocks(E, N, days):
+    """Many consecutive reference-RNG days: numpy's stream of every env crosses its 624-word blocks in
+    every way the device keeps it (mt_prepare_kernel: a twist, or none when the other block already
+    holds the successor (kMtNextReady); a day that draws past both prepared blocks twists on its lane --
+    N = 50 and 128 draw more than 624 words a day).  Obs and rewards bit-exact against the oracle's
+    RandomState-equal streams, day after day (charging_station.py:200-279)."""
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
+              battery_system_available_in_model=True)
+    seed = 77 + N
+    O.lib().orc_set_square_mode(1)
+    venv = SmartNanogridVecEnv(E, seed=seed, rng="reference", **kw)
+    cfg, envs = _oracle_batch(kw, seed, range(E))
+    rng = np.random.default_rng(days + N)
+    obs = venv.reset()
+    for day in range(days):
+        np.testing.assert_array_equal(obs, np.stack([e.reset() for e in envs]), err_msg=f"day{day} t=0")
+        for t in range(cfg.T):
+            a = rng.uniform(venv.action_space.low, venv.action_space.high, (E, venv.act_dim)).astype(np.float32)
+            obs, rew, dones, infos = venv.step(a)
+            outs = [e.step(a[i]) for i, e in enumerate(envs)]
+            got = np.stack([inf.get("terminal_observation", obs[i]) for i, inf in enumerate(infos)])
+            np.testing.assert_array_equal(got, np.stack([o[0] for o in outs]), err_msg=f"day{day} t{t}")
+            np.testing.assert_array_equal(rew, np.array([o[1] for o in outs]), err_msg=f"day{day} t{t}")
+    venv.close()
+
+
 def test_full_size_sampled_parity_65536():
     """Config 3 size (65,536 envs x 10 chargers) with reference RNG: 512 sampled envs against the oracle,
     plus size-independent invariants on all envs."""
