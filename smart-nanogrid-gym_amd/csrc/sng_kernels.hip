@@ -1798,18 +1798,62 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
 
 // One env's numpy stream inside ref_day_kernel: RandomState.random_sample / uniform / randint
 // (legacy, masked rejection) over the tempered words of the prepared blocks (sng_mt.h, host twin).
-struct MtLane {
+//
+// The words reach the lane through a ring of 64 words in LDS, topped up for the whole wavefront at
+// once: the draws of a day are data-dependent (a free step draws two words, an arrival ~10), so the
+// 64 lanes of a wavefront desynchronise, and a global load per draw made every draw of every lane
+// wait out a memory round trip (0.53 ms per day at any population size).  Now a lane's draw is an
+// LDS read; when any lane's ring holds <= 32 words, every lane refills its ring to 64 with loads
+// issued together and one wait, ~20 times a day.  A draw that finds the ring empty (a rejection
+// streak) loads its word directly.
+// Word a of the day (a = 0: the first draw) is word q = mti0 + a of the stream from the current
+// block: block k = q / 624 sits in slot (cur0 + k) & 1.  Blocks 0 and 1 are prepared
+// (mt_prepare_kernel); a day that draws into block 2 or beyond twists it on its lane into the slot of
+// block k - 2, which the ring has consumed by then (it runs at most 64 words ahead).
+constexpr int kRing = 64;
+struct MtRing {
     uint32_t *blk;
-    int cur, mti;
-    bool ready;   // the other block holds the next state (set by mt_prepare_kernel)
-    __device__ __forceinline__ uint32_t next() {
-        if (mti >= kMtN) {
-            if (!ready) mt_twist_lane(blk + cur * kMtN, blk + (cur ^ 1) * kMtN);
-            cur ^= 1;
-            mti = 0;
-            ready = false;
+    uint32_t *ring;   // this lane's ring: ring[j * kWave], j < kRing
+    int cur0, mti0;
+    int head, tail;   // words drawn / words loaded into the ring, counted from the day's first
+    int avail;        // stream blocks materialised: 0 .. avail - 1
+    __device__ __forceinline__ const uint32_t *word_ptr(int a) const {
+        const int q = mti0 + a, k = q / kMtN;
+        return blk + ((cur0 + k) & 1) * kMtN + (q - k * kMtN);
+    }
+    __device__ __forceinline__ void materialise(int last) {   // blocks up to that of word `last`
+        const int kmax = (mti0 + last) / kMtN;
+        while (avail <= kmax) {   // rare: a day of more than ~1,000 draws
+            mt_twist_lane(blk + ((cur0 + avail - 1) & 1) * kMtN, blk + ((cur0 + avail) & 1) * kMtN);
+            ++avail;
         }
-        return mt_temper(blk[cur * kMtN + mti++]);
+    }
+    // wave-uniform: every lane tops its ring up to kRing words (called by all lanes of the wavefront)
+    __device__ __forceinline__ void refill() {
+        const int count = kRing - (tail - head);
+        if (count > 0) materialise(tail + count - 1);
+        uint32_t x[kRing];
+#pragma unroll
+        for (int j = 0; j < kRing; ++j) x[j] = j < count ? *word_ptr(tail + j) : 0u;
+#pragma unroll
+        for (int j = 0; j < kRing; ++j)
+            if (j < count) ring[((tail + j) & (kRing - 1)) * kWave] = x[j];
+        tail += count > 0 ? count : 0;
+    }
+    __device__ __forceinline__ void top_up() {
+        if (__builtin_amdgcn_ballot_w64(tail - head <= kRing / 2)) refill();
+    }
+    __device__ __forceinline__ uint32_t next() {
+        uint32_t y;
+        if (head < tail) {
+            y = ring[(head & (kRing - 1)) * kWave];
+        } else {   // the ring ran dry inside one step: this word straight from the stream
+            materialise(head);
+            y = *word_ptr(head);
+            tail = head + 1;
+        }
+        ++head;
+        return mt_temper(y);
     }
     __device__ __forceinline__ double random() {
         const int32_t a = (int32_t)(next() >> 5), b = (int32_t)(next() >> 6);
@@ -1830,16 +1874,28 @@ struct MtLane {
         }
         return low + (int)v;
     }
+    // the stream position after the day, as MtLane kept it: the block of the last word drawn and the
+    // words drawn from it (624 = exhausted, twisted lazily at the next draw); kMtNextReady when the
+    // other slot holds that block's successor
+    __device__ __forceinline__ int32_t position() const {
+        if (head == 0) return (cur0 << 16) | kMtNextReady | mti0;
+        const int q = mti0 + head, k = (q - 1) / kMtN;
+        return (((cur0 + k) & 1) << 16) | (k + 1 < avail ? kMtNextReady : 0) | (q - k * kMtN);
+    }
 };
 
 // The day of every env: generate_day + encode_day (sng_api.cpp) on one thread per env, charger by
 // charger; the lanes of a wavefront step (charger, t) together, so the timeline stores coalesce.
-__global__ __launch_bounds__(256) void ref_day_kernel(Params p, DeviceState s, RefStreams rs, int64_t E, int i4,
-                                                      int i10, int i1) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= E) return;
+constexpr int kRefBlock = kWave;   // one wavefront per workgroup: its rings are 16 KB of LDS
+__global__ __launch_bounds__(kRefBlock) void ref_day_kernel(Params p, DeviceState s, RefStreams rs, int64_t E, int i4,
+                                                            int i10, int i1) {
+    __shared__ uint32_t rings[kRing * kWave];
+    const int lane = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * kRefBlock;
+    const bool live = e0 + lane < E;
+    const int64_t e = live ? e0 + lane : E - 1;   // idle lanes follow env E - 1's stream and store nothing
     const int32_t pos = rs.pos[e];
-    MtLane rng{rs.mt + (size_t)e * 2 * kMtN, (pos >> 16) & 1, pos & kMtPosMask, true};
+    MtRing rng{rs.mt + (size_t)e * 2 * kMtN, rings + lane, (pos >> 16) & 1, pos & kMtPosMask, 0, 0, 2};
     const int T = p.T, n = p.n;
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;   // as generate_kernel
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
@@ -1852,9 +1908,19 @@ __global__ __launch_bounds__(256) void ref_day_kernel(Params p, DeviceState s, R
         uint32_t cur_cap = 0;
         double cur_req = 0.0, prev_req = 0.0;
         for (int t = 0; t < T; ++t) {
+            rng.top_up();   // wave-uniform
             bool arrived = false;
             double soc_arr = 0.0;
             if (!present) {
+#ifdef SNG_RD_NODRAW   // diagnostic builds only (timing breakdown of this kernel): no stream draws
+                const double r = (double)((e * 2654435761u + c * 97u + t * 31u) & 1023u) / 1024.0;
+                if ((r - 0.1) > 0.5) {
+                    present = arrived = true;
+                    soc_arr = 0.5;
+                    cur_cap = 40u;
+                    dep = t + i4 + 1;
+                }
+#else
                 const double r = rng.random();
                 if ((r - 0.1) > 0.5) {   // round(random.rand() - 0.1) == 1 (charging_station.py:214-215)
                     present = arrived = true;
@@ -1866,6 +1932,7 @@ __global__ __launch_bounds__(256) void ref_day_kernel(Params p, DeviceState s, R
                     const int high = min(t + i10, T + i1), low = t + i4;       // :271-279
                     dep = (low >= high) ? low : rng.randint(low, high);
                 }
+#endif
             }
             const bool occ = present && t < dep;
             if (!occ) present = false;
@@ -1874,17 +1941,23 @@ __global__ __launch_bounds__(256) void ref_day_kernel(Params p, DeviceState s, R
             const int rem = occ ? dep - t : 0;
             const bool pen = (uint32_t)prev_rem - pen_lo <= pen_span;   // prev_rem = 0: empty at t-1
             const size_t plane = (size_t)t * n * (size_t)E;
-            bst(s.word + plane, el4, pack_word(occ, !running, pen, occ ? cur_cap : 0u, (uint32_t)rem), r4);
-            bst(s.aux + plane, el8, (occ && !running) ? soc_arr : 0.0, r8);
-            // Requested_SOC[c, t-1]; slot 0 holds Requested_SOC[c, T-1] (written after the loop)
-            if (p.req_stream && t > 0) bst(s.req + plane, el8, prev_req, r8);
+#ifdef SNG_RD_NOSTORE   // diagnostic builds only: the day's draws without its timeline stores
+            if (live && soc_arr == 12345.0) {
+#else
+            if (live) {
+#endif
+                bst(s.word + plane, el4, pack_word(occ, !running, pen, occ ? cur_cap : 0u, (uint32_t)rem), r4);
+                bst(s.aux + plane, el8, (occ && !running) ? soc_arr : 0.0, r8);
+                // Requested_SOC[c, t-1]; slot 0 holds Requested_SOC[c, T-1] (written after the loop)
+                if (p.req_stream && t > 0) bst(s.req + plane, el8, prev_req, r8);
+            }
             prev_occ = occ;
             prev_rem = rem;
             prev_req = occ ? cur_req : 0.0;
         }
-        if (p.req_stream) bst(s.req, el8, prev_req, r8);
+        if (live && p.req_stream) bst(s.req, el8, prev_req, r8);
     }
-    rs.pos[e] = (rng.cur << 16) | (rng.ready ? kMtNextReady : 0) | rng.mti;   // no block switch: the successor stays
+    if (live) rs.pos[e] = rng.position();
 }
 
 hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream) {
@@ -1899,8 +1972,8 @@ hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStream
     hipLaunchKernelGGL(mt_prepare_kernel, dim3((unsigned)((E + 3) / 4)), dim3(256), 0, stream, rs, E);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ref_day_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, p, s, rs, E, i4,
-                       i10, i1);
+    hipLaunchKernelGGL(ref_day_kernel, dim3((unsigned)((E + kRefBlock - 1) / kRefBlock)), dim3(kRefBlock), 0, stream, p,
+                       s, rs, E, i4, i10, i1);
     return hipGetLastError();
 }
 
