@@ -1799,59 +1799,66 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
 // One env's numpy stream inside ref_day_kernel: RandomState.random_sample / uniform / randint
 // (legacy, masked rejection) over the tempered words of the prepared blocks (sng_mt.h, host twin).
 //
-// The words reach the lane through a ring of 64 words in LDS, topped up for the whole wavefront at
+// The words reach the lane through a ring of 128 words in LDS, topped up for the whole wavefront at
 // once: the draws of a day are data-dependent (a free step draws two words, an arrival ~10), so the
 // 64 lanes of a wavefront desynchronise, and a global load per draw made every draw of every lane
 // wait out a memory round trip (0.53 ms per day at any population size).  Now a lane's draw is an
-// LDS read; when any lane's ring holds <= 32 words, every lane refills its ring to 64 with loads
-// issued together and one wait, ~20 times a day.  A draw that finds the ring empty (a rejection
-// streak) loads its word directly.
-// Word a of the day (a = 0: the first draw) is word q = mti0 + a of the stream from the current
-// block: block k = q / 624 sits in slot (cur0 + k) & 1.  Blocks 0 and 1 are prepared
-// (mt_prepare_kernel); a day that draws into block 2 or beyond twists it on its lane into the slot of
-// block k - 2, which the ring has consumed by then (it runs at most 64 words ahead).
-constexpr int kRing = 64;
+// LDS read; when any lane's ring holds <= 32 words, every lane holding <= 64 loads the next 64 words
+// (16 aligned 16 B loads issued together, one wait), ~10-15 times a day.  A draw that finds the ring
+// empty (a rejection streak) loads its word directly.
+// Stream word q counts from the start of the day's current block: block k = q / 624 sits in slot
+// (cur0 + k) & 1, and a 4-word group never straddles two blocks (624 = 4 * 156).  Blocks 0 and 1 are
+// prepared (mt_prepare_kernel); a day that draws into block 2 or beyond twists it on its lane into the
+// slot of block k - 2, which the ring has consumed by then (it runs at most 128 words ahead).
+// LDS layout ring[slot][lane]: lanes reading any slots hit distinct banks.
+constexpr int kRing = 128;
 struct MtRing {
     uint32_t *blk;
-    uint32_t *ring;   // this lane's ring: ring[j * kWave], j < kRing
-    int cur0, mti0;
-    int head, tail;   // words drawn / words loaded into the ring, counted from the day's first
+    uint32_t *ring;   // this lane's ring: ring[slot * kWave], slot < kRing
+    int cur0;
+    int head, tail;   // stream words (from the current block's start) drawn / loaded into the ring
+    int q0;           // the day's first word (mti at the start)
     int avail;        // stream blocks materialised: 0 .. avail - 1
-    __device__ __forceinline__ const uint32_t *word_ptr(int a) const {
-        const int q = mti0 + a, k = q / kMtN;
+    __device__ __forceinline__ const uint32_t *word_ptr(int q) const {
+        const int k = q / kMtN;
         return blk + ((cur0 + k) & 1) * kMtN + (q - k * kMtN);
     }
     __device__ __forceinline__ void materialise(int last) {   // blocks up to that of word `last`
-        const int kmax = (mti0 + last) / kMtN;
+        const int kmax = last / kMtN;
         while (avail <= kmax) {   // rare: a day of more than ~1,000 draws
             mt_twist_lane(blk + ((cur0 + avail - 1) & 1) * kMtN, blk + ((cur0 + avail) & 1) * kMtN);
             ++avail;
         }
     }
-    // wave-uniform: every lane tops its ring up to kRing words (called by all lanes of the wavefront)
+    // wave-uniform: lanes holding <= 64 words load the next 64 (tail stays a multiple of 4)
     __device__ __forceinline__ void refill() {
-        const int count = kRing - (tail - head);
-        if (count > 0) materialise(tail + count - 1);
-        uint32_t x[kRing];
+        if (tail - head <= kRing / 2) {
+            materialise(tail + kRing / 2 - 1);
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            u32x4 x[kRing / 8];
 #pragma unroll
-        for (int j = 0; j < kRing; ++j) x[j] = j < count ? *word_ptr(tail + j) : 0u;
+            for (int g = 0; g < kRing / 8; ++g) x[g] = *reinterpret_cast<const u32x4 *>(word_ptr(tail + 4 * g));
 #pragma unroll
-        for (int j = 0; j < kRing; ++j)
-            if (j < count) ring[((tail + j) & (kRing - 1)) * kWave] = x[j];
-        tail += count > 0 ? count : 0;
+            for (int g = 0; g < kRing / 8; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) ring[((tail + 4 * g + i) & (kRing - 1)) * kWave] = x[g][i];
+            tail += kRing / 2;
+        }
     }
     __device__ __forceinline__ void top_up() {
-        if (__builtin_amdgcn_ballot_w64(tail - head <= kRing / 2)) refill();
+        if (__builtin_amdgcn_ballot_w64(tail - head <= kRing / 4)) refill();
     }
     __device__ __forceinline__ uint32_t next() {
-        uint32_t y;
-        if (head < tail) {
-            y = ring[(head & (kRing - 1)) * kWave];
-        } else {   // the ring ran dry inside one step: this word straight from the stream
+        if (head >= tail) {   // the ring ran dry inside one step: the word's aligned group straight in
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             materialise(head);
-            y = *word_ptr(head);
-            tail = head + 1;
+            const int g = head & ~3;
+            const u32x4 x = *reinterpret_cast<const u32x4 *>(word_ptr(g));
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ring[((g + i) & (kRing - 1)) * kWave] = x[i];
+            tail = g + 4;
         }
+        const uint32_t y = ring[(head & (kRing - 1)) * kWave];
         ++head;
         return mt_temper(y);
     }
@@ -1878,15 +1885,15 @@ struct MtRing {
     // words drawn from it (624 = exhausted, twisted lazily at the next draw); kMtNextReady when the
     // other slot holds that block's successor
     __device__ __forceinline__ int32_t position() const {
-        if (head == 0) return (cur0 << 16) | kMtNextReady | mti0;
-        const int q = mti0 + head, k = (q - 1) / kMtN;
-        return (((cur0 + k) & 1) << 16) | (k + 1 < avail ? kMtNextReady : 0) | (q - k * kMtN);
+        if (head == q0) return (cur0 << 16) | kMtNextReady | q0;
+        const int k = (head - 1) / kMtN;
+        return (((cur0 + k) & 1) << 16) | (k + 1 < avail ? kMtNextReady : 0) | (head - k * kMtN);
     }
 };
 
 // The day of every env: generate_day + encode_day (sng_api.cpp) on one thread per env, charger by
 // charger; the lanes of a wavefront step (charger, t) together, so the timeline stores coalesce.
-constexpr int kRefBlock = kWave;   // one wavefront per workgroup: its rings are 16 KB of LDS
+constexpr int kRefBlock = kWave;   // one wavefront per workgroup: its rings are 32 KB of LDS
 __global__ __launch_bounds__(kRefBlock) void ref_day_kernel(Params p, DeviceState s, RefStreams rs, int64_t E, int i4,
                                                             int i10, int i1) {
     __shared__ uint32_t rings[kRing * kWave];
@@ -1895,7 +1902,8 @@ __global__ __launch_bounds__(kRefBlock) void ref_day_kernel(Params p, DeviceStat
     const bool live = e0 + lane < E;
     const int64_t e = live ? e0 + lane : E - 1;   // idle lanes follow env E - 1's stream and store nothing
     const int32_t pos = rs.pos[e];
-    MtRing rng{rs.mt + (size_t)e * 2 * kMtN, rings + lane, (pos >> 16) & 1, pos & kMtPosMask, 0, 0, 2};
+    const int mti = pos & kMtPosMask;
+    MtRing rng{rs.mt + (size_t)e * 2 * kMtN, rings + lane, (pos >> 16) & 1, mti, mti & ~3, mti, 2};
     const int T = p.T, n = p.n;
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;   // as generate_kernel
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
