@@ -1812,9 +1812,17 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
 // slot of block k - 2, which the ring has consumed by then (it runs at most 128 words ahead).
 // LDS layout ring[slot][lane]: lanes reading any slots hit distinct banks.
 constexpr int kRing = 128;
+// Envs per wavefront (lanes >= kRefEnvs mirror lane % kRefEnvs: same stream, same branches, nothing
+// stored).  64 at 65,536 envs: 32 / 16 / 8 envs per wavefront ran the day in 338 / 405 / 505 us against
+// 331 us (rocprof, one box) -- the kernel is bound by the instructions the divergent wavefronts issue,
+// not by the latency more wavefronts would hide; at 4,096 envs 8 per wavefront is faster (193 vs 277 us).
+#ifndef SNG_REF_ENVS
+#define SNG_REF_ENVS 64
+#endif
+constexpr int kRefEnvs = SNG_REF_ENVS;
 struct MtRing {
     uint32_t *blk;
-    uint32_t *ring;   // this lane's ring: ring[slot * kWave], slot < kRing
+    uint32_t *ring;   // this lane's ring: ring[slot * kRefEnvs], slot < kRing
     int cur0;
     int head, tail;   // stream words (from the current block's start) drawn / loaded into the ring
     int q0;           // the day's first word (mti at the start)
@@ -1841,7 +1849,7 @@ struct MtRing {
 #pragma unroll
             for (int g = 0; g < kRing / 8; ++g)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ring[((tail + 4 * g + i) & (kRing - 1)) * kWave] = x[g][i];
+                for (int i = 0; i < 4; ++i) ring[((tail + 4 * g + i) & (kRing - 1)) * kRefEnvs] = x[g][i];
             tail += kRing / 2;
         }
     }
@@ -1855,10 +1863,10 @@ struct MtRing {
             const int g = head & ~3;
             const u32x4 x = *reinterpret_cast<const u32x4 *>(word_ptr(g));
 #pragma unroll
-            for (int i = 0; i < 4; ++i) ring[((g + i) & (kRing - 1)) * kWave] = x[i];
+            for (int i = 0; i < 4; ++i) ring[((g + i) & (kRing - 1)) * kRefEnvs] = x[i];
             tail = g + 4;
         }
-        const uint32_t y = ring[(head & (kRing - 1)) * kWave];
+        const uint32_t y = ring[(head & (kRing - 1)) * kRefEnvs];
         ++head;
         return mt_temper(y);
     }
@@ -1867,6 +1875,15 @@ struct MtRing {
         return (a * 67108864.0 + b) / 9007199254740992.0;
     }
     __device__ __forceinline__ double uniform(double lo, double hi) { return lo + (hi - lo) * random(); }
+    // a draw whose value is discarded (a uniform: two words) only advances the stream
+    __device__ __forceinline__ void skip2() {
+        if (head + 2 <= tail) {
+            head += 2;
+        } else {
+            (void)next();
+            (void)next();
+        }
+    }
     __device__ __forceinline__ int randint(int low, int high) {   // exclusive high; one value: no draw
         if (high - 1 - low == 0) return low;
         uint32_t mask = (uint32_t)(high - 1 - low);
@@ -1893,14 +1910,14 @@ struct MtRing {
 
 // The day of every env: generate_day + encode_day (sng_api.cpp) on one thread per env, charger by
 // charger; the lanes of a wavefront step (charger, t) together, so the timeline stores coalesce.
-constexpr int kRefBlock = kWave;   // one wavefront per workgroup: its rings are 32 KB of LDS
+constexpr int kRefBlock = kWave;   // one wavefront per workgroup, kRefEnvs envs: its rings are kRefEnvs x 512 B of LDS
 __global__ __launch_bounds__(kRefBlock) void ref_day_kernel(Params p, DeviceState s, RefStreams rs, int64_t E, int i4,
                                                             int i10, int i1) {
-    __shared__ uint32_t rings[kRing * kWave];
-    const int lane = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * kRefBlock;
-    const bool live = e0 + lane < E;
-    const int64_t e = live ? e0 + lane : E - 1;   // idle lanes follow env E - 1's stream and store nothing
+    __shared__ uint32_t rings[kRing * kRefEnvs];
+    const int lane = threadIdx.x % kRefEnvs;   // the env slot; lanes >= kRefEnvs mirror it
+    const int64_t e0 = (int64_t)blockIdx.x * kRefEnvs;
+    const bool live = e0 + lane < E && (int)threadIdx.x < kRefEnvs;
+    const int64_t e = e0 + lane < E ? e0 + lane : E - 1;   // past E: env E - 1's stream, nothing stored
     const int32_t pos = rs.pos[e];
     const int mti = pos & kMtPosMask;
     MtRing rng{rs.mt + (size_t)e * 2 * kMtN, rings + lane, (pos >> 16) & 1, mti, mti & ~3, mti, 2};
@@ -1934,7 +1951,7 @@ __global__ __launch_bounds__(kRefBlock) void ref_day_kernel(Params p, DeviceStat
                     present = arrived = true;
                     soc_arr = rng.uniform(0.1, 0.9);                            // :257-259
                     const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
-                    (void)rng.uniform(lo, 1.0);                                 // discarded draw, :219
+                    rng.skip2();                                                // discarded uniform, :219
                     cur_cap = p.diff_caps ? (uint32_t)rng.randint(15, 120) : 40u;   // :267-269
                     cur_req = p.req_enabled ? rng.uniform(lo, 1.0) : 1.0;       // :261-265
                     const int high = min(t + i10, T + i1), low = t + i4;       // :271-279
@@ -1980,7 +1997,7 @@ hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStream
     hipLaunchKernelGGL(mt_prepare_kernel, dim3((unsigned)((E + 3) / 4)), dim3(256), 0, stream, rs, E);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ref_day_kernel, dim3((unsigned)((E + kRefBlock - 1) / kRefBlock)), dim3(kRefBlock), 0, stream, p,
+    hipLaunchKernelGGL(ref_day_kernel, dim3((unsigned)((E + kRefEnvs - 1) / kRefEnvs)), dim3(kRefBlock), 0, stream, p,
                        s, rs, E, i4, i10, i1);
     return hipGetLastError();
 }

@@ -5,7 +5,7 @@
 #   make -C smart-nanogrid-gym_amd/csrc variants VARIANTS="rdnodraw:-DSNG_RD_NODRAW rdnostore:-DSNG_RD_NOSTORE"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for l in libsng libsng_rdnodraw libsng_rdnostore; do
+for l in ${RD_LIBS:-libsng libsng_rdnodraw libsng_rdnostore}; do
   SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/rd_$l \
     -o run --output-format csv -- python tools/reset_bench.py --repeats 3 > gpurun_out/rd_$l.log 2>&1 || exit $?
   python3 - "$l" <<'PY'
