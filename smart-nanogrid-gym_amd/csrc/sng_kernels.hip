@@ -1207,26 +1207,38 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
         const uint32_t *__restrict__ word = s.word;
         const double *__restrict__ auxv = s.aux;
         double *__restrict__ socv = s.soc;
-        // batches of 8 chargers: all loads of a batch issued before its stores (t = 0 slice)
-        for (int c0 = 0; c0 < n; c0 += 8) {
-            uint32_t w[8];
-            double aux[8];
+        // batches of 16 chargers: all loads of a batch issued before its stores (t = 0 slice); a packed
+        // day's two planes are both loaded up front (the plane-0 record is used only where plane 1 is
+        // occupied), so a batch is one memory round trip (config-5 reset 293 -> 257 us, A/B)
+        constexpr int B = 16;
+        for (int c0 = 0; c0 < n; c0 += B) {
+            uint32_t w[B];
+            double aux[B];
+            if (PK) {   // packed device-day records (sng_layout.h): t = 0 is plane 1; plane 0 carries
+                        // the SoC of the t = 0 arrivals
+                const uint32_t *rec = reinterpret_cast<const uint32_t *>(auxv);
+                uint32_t r0[B], r1[B];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int c = c0 + j < n ? c0 + j : n - 1;
-                if (PK) {   // packed device-day records (sng_layout.h): t = 0 is plane 1; plane 0 carries
-                            // the SoC of the t = 0 arrivals
-                    const uint32_t *rec = reinterpret_cast<const uint32_t *>(auxv);
-                    const uint32_t r = rec[((size_t)n + c) * E + e];
-                    w[j] = (r & W_OCC) ? r : 0u;   // an empty charger's record carries a SoC, not a departure
-                    aux[j] = (r & W_OCC) ? (double)rec_soc(rec[(size_t)c * E + e]) : 0.0;
-                } else {
+                for (int j = 0; j < B; ++j) {
+                    const int c = c0 + j < n ? c0 + j : n - 1;
+                    r1[j] = rec[((size_t)n + c) * E + e];
+                    r0[j] = rec[(size_t)c * E + e];
+                }
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    w[j] = (r1[j] & W_OCC) ? r1[j] : 0u;   // an empty charger's record carries a SoC, not a departure
+                    aux[j] = (r1[j] & W_OCC) ? (double)rec_soc(r0[j]) : 0.0;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < B; ++j) {
+                    const int c = c0 + j < n ? c0 + j : n - 1;
                     w[j] = word[(size_t)c * E + e];
                     aux[j] = auxv[(size_t)c * E + e];
                 }
             }
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < B; ++j) {
                 const int c = c0 + j;
                 if (c < n) {
                     SNG_ST(socv[(size_t)c * E + e], aux[j]);
