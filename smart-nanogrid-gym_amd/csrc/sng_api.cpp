@@ -439,6 +439,38 @@ uint64_t fnv1a(const void *data, size_t n, uint64_t h = 1469598103934665603ull) 
     return h;
 }
 
+// The checkpoint's configuration fingerprint: every SngConfig field that changes the simulation, hashed
+// field by field (the struct's padding and -0.0 vs 0.0 must not make an identical configuration differ
+// across processes or bindings).  The irradiance enters through the tables, hashed next to it.
+uint64_t config_fingerprint(const SngConfig &c) {
+    uint64_t h = 1469598103934665603ull;
+    auto i32 = [&h](int32_t v) { h = fnv1a(&v, sizeof v, h); };
+    auto f64 = [&h](double v) {
+        if (v == 0.0) v = 0.0;   // -0.0 -> 0.0
+        h = fnv1a(&v, sizeof v, h);
+    };
+    i32(c.abi_version);
+    i32(c.number_of_chargers);
+    f64(c.time_interval_hours);
+    i32(c.price_model);
+    i32(c.pv_system_available);
+    i32(c.battery_system_available);
+    i32(c.vehicle_to_everything);
+    i32(c.different_vehicle_capacities);
+    i32(c.requested_state_of_charge);
+    i32(c.charging_mode_bounded);
+    i32(c.penalty_mode);
+    i32(c.numpy_legacy_promotion);
+    for (double v : {c.grid_cost_weight, c.battery_penalty_weight, c.selling_price_coefficient, c.bess_capacity_kwh,
+                     c.bess_initial_soc, c.bess_max_charging_kw, c.bess_max_discharging_kw, c.bess_charging_efficiency,
+                     c.bess_discharging_efficiency, c.bess_depth_of_discharge, c.ev_max_power_kw, c.ev_efficiency})
+        f64(v);
+    i32(c.extended_day);
+    f64(c.pv_noise);
+    f64(c.price_noise);
+    return h;
+}
+
 }  // namespace
 
 struct SngEnv {
@@ -490,6 +522,10 @@ struct SngGraph {
     SngEnv *env = nullptr;
     bool with_reset = false;
     DayKey key{};   // the loaded-day encoding the graph's steps were captured for
+    // the stream keys baked into the captured kernels' arguments: the device days a reset graph draws
+    // and the PV-ratio / profile streams are those of this seed and env offset
+    uint64_t seed = 0;
+    int64_t env_offset = 0;
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
 };
@@ -897,15 +933,8 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
     }
     ht.recip[0] = 0.0;
     for (int c = 1; c < 256; ++c) ht.recip[c] = 1.0 / (double)c;
-    {
-        // checkpoint fingerprint: every configuration scalar that changes the simulation, and the tables
-        SngConfig k = c;
-        k.irradiance_per_minute = nullptr;
-        k.irradiance_minutes = 0;
-        k.step_lanes_per_env = 0;
-        k.reserved0 = 0;
-        env->cfg_hash = fnv1a(&ht, sizeof ht, fnv1a(&k, sizeof k));
-    }
+    // checkpoint fingerprint: every configuration scalar that changes the simulation, and the tables
+    env->cfg_hash = fnv1a(&ht, sizeof ht, config_fingerprint(c));
 
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) {
@@ -1072,6 +1101,10 @@ int sng_reset_replay(SngEnv *env, float *obs, void *stream) {
     HIP_TRY(env, hipSetDevice(env->device));
     hipStream_t st = as_stream(stream);
     const int vec = aligned16(obs) ? 1 : 0;
+    // a device day is counted by its first step; one replayed before any step was never counted, and
+    // the replay's steps do not count (bump_day = 0 below), so count it here, as sng_reset does for a
+    // second device reset in a row: the next device reset then draws a new day
+    if (env->p.packed && env->p.bump_day && env->t == 0) HIP_TRY(env, launch_bump_day(env->ds, st));
     if (env->gen_mode == SNG_RNG_REFERENCE) {
         // a new random_pv_shift_ratio from each env's Python stream (smart_nanogrid_environment.py:349),
         // after the day-end draw the last step still owes (:181); the numpy stream is not touched
@@ -1141,7 +1174,16 @@ int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void
                               }
                               return true;
                           });
-    if (rc) return rc;
+    if (rc) {
+        // chunks before the failing env are already uploaded over the loaded day's planes and their
+        // Python-stream draws consumed: the loaded day is no longer valid, so step, replay and
+        // steps-only graphs refuse until the next reset
+        env->t = -1;
+        env->gen_loaded = false;
+        env->day_finished = false;
+        env->err += " (the loaded day was partly overwritten: reset again)";
+        return rc;
+    }
     rc = finish_host_day(env, req_enabled || need, obs, as_stream(stream));
     if (rc) return rc;
     env->gen_loaded = false;   // the generated day a replay restores is no longer loaded
@@ -1387,6 +1429,18 @@ struct StateHeader {
 };
 static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '2'};
 
+// The blob's size for this handle and the header's section flags.
+static uint64_t state_bytes(const SngEnv *env, const StateHeader &h) {
+    const size_t E = (size_t)env->E, tl = env->timeline();
+    size_t b = sizeof(StateHeader) + (size_t)env->p.n * E * 8 + 4 * E * 8 + E * 4 + tl * 8;
+    if (h.has_word) b += tl * 4;
+    if (h.has_req) b += tl * 8;
+    if (h.has_prof) b += 2 * (size_t)(env->p.T + 3) * E * 8;
+    if (h.has_return) b += E * 8;
+    if (h.has_streams) b += E * 2 * MT19937::kStateWords * 4;
+    return b;
+}
+
 static StateHeader state_layout(const SngEnv *env, bool with_return) {
     StateHeader h{};
     std::memcpy(h.magic, kStateMagic, sizeof h.magic);
@@ -1414,14 +1468,7 @@ static StateHeader state_layout(const SngEnv *env, bool with_return) {
     h.has_prof = env->ds.prof ? 1 : 0;
     h.has_return = with_return ? 1 : 0;
     h.has_streams = env->py_rng.empty() ? 0 : 1;
-    const size_t E = (size_t)env->E, tl = env->timeline();
-    size_t b = sizeof(StateHeader) + (size_t)env->p.n * E * 8 + 4 * E * 8 + E * 4 + tl * 8;
-    if (h.has_word) b += tl * 4;
-    if (h.has_req) b += tl * 8;
-    if (h.has_prof) b += 2 * (size_t)(env->p.T + 3) * E * 8;
-    if (h.has_return) b += E * 8;
-    if (h.has_streams) b += E * 2 * MT19937::kStateWords * 4;
-    h.total_bytes = b;
+    h.total_bytes = state_bytes(env, h);
     return h;
 }
 
@@ -1494,6 +1541,11 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
     if (h.num_envs != env->E || h.n != env->p.n || h.T != env->p.T || h.slots != env->slots ||
         h.obs_dim != env->p.obs_dim || h.config_hash != env->cfg_hash)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "state of a handle with another configuration or size");
+    // the sections the header announces must be self-consistent before any of them is read
+    auto flag = [](int32_t v) { return v == 0 || v == 1; };
+    if (!flag(h.has_word) || !flag(h.has_req) || !flag(h.has_prof) || !flag(h.has_return) || !flag(h.has_streams) ||
+        !flag(h.packed) || h.has_word != 1 - h.packed || state_bytes(env, h) != h.total_bytes)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT, "corrupt state header (inconsistent sections or size)");
     if (h.total_bytes > bytes) return fail(env, SNG_ERR_INVALID_ARGUMENT, "truncated state");
     if (h.has_return && !episode_return)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "the state holds day returns: pass an episode_return array");
@@ -1597,6 +1649,8 @@ int sng_graph_create(SngEnv *env, const float *actions, float *obs, double *rewa
     }
     g->with_reset = with_reset;
     g->key = day_key(p);
+    g->seed = env->seed;
+    g->env_offset = p.env_offset;
     const InfoPtrs ip = info_ptrs(info);
     const int64_t E = env->E;
     const int A = p.act_dim;
@@ -1636,8 +1690,11 @@ int sng_graph_launch(SngGraph *g, void *stream) {
                         "graph captured for a day of another encoding (RNG mode, requested-SoC stream or replay): "
                         "recapture it after this reset");
         if (env->t != 0) return fail(env, SNG_ERR_STATE, "a steps-only graph starts at t = 0: reset first");
-        if (env->seed != env->p.seed) return fail(env, SNG_ERR_STATE, "seed changed since capture");
     }
+    // sng_set_seed / sng_set_state / sng_set_env_offset since the capture: the graph's kernels would
+    // still draw the old streams
+    if (g->seed != env->seed || g->env_offset != env->p.env_offset)
+        return fail(env, SNG_ERR_STATE, "seed or env offset changed since the graph was captured: recapture it");
     HIP_TRY(env, hipSetDevice(env->device));
     // the graph's first reset must not redraw a device day that was reset but never stepped
     if (g->with_reset && env->p.packed && env->p.bump_day && env->t == 0)

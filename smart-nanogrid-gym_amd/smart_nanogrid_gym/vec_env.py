@@ -1,11 +1,18 @@
 """Batched SmartNanogridEnv: num_envs independent copies of the reference environment
 stepped by one fused HIP kernel per timestep (libsng.so).
 
-`SmartNanogridVecEnv` duck-types stable-baselines3's VecEnv (reset / step_async /
-step_wait / num_envs / observation_space / action_space / get_attr / set_attr /
-env_method / env_is_wrapped / seed / close) with the DummyVecEnv conventions: automatic
-reset at the end of the day and the final observation in infos[i]['terminal_observation'].
-`reset_tensors` / `step_tensors` keep everything on the GPU for device-resident RL loops.
+`SmartNanogridVecEnv` is a stable-baselines3 VecEnv: it subclasses
+`stable_baselines3.common.vec_env.VecEnv` when SB3 is importable (SB3's BaseAlgorithm._wrap_env
+takes an env as batched only through `isinstance(env, VecEnv)`, and wraps anything else in a
+DummyVecEnv as ONE env -- solvers/RL/ppo_train.py:89-92), and `object` otherwise, as envs.py does
+for gym.Env.  It follows SB3 2.x's VecEnv contract (reset / step_async / step_wait / get_attr /
+set_attr / env_method / env_is_wrapped / seed / set_options / close, `reset_infos`) with the
+DummyVecEnv conventions: seeds and options given by seed() / set_options() apply at the next
+reset(), automatic reset at the end of the day and the final observation in
+infos[i]['terminal_observation'].  SB3 is not installed in this image, so the SB3 runtime itself is
+parity-unpinned; tests/test_vecenv_sb3_cpu.py checks the hierarchy against a stand-in of SB3 2.x's
+abstract VecEnv.  `reset_tensors` / `step_tensors` keep everything on the GPU for device-resident
+RL loops.
 
 Reference behaviour mirrored per env (smart_nanogrid_gym/envs/smart_nanogrid_environment.py):
   reset()  -> new day, t = 0, BESS state of charge carried over (:311-351)
@@ -28,6 +35,11 @@ try:
 except Exception:  # pragma: no cover
     torch = None
 
+try:  # SB3 attaches a batched env only when it is an instance of its VecEnv
+    from stable_baselines3.common.vec_env import VecEnv as _VecEnvBase   # pragma: no cover - not in the image
+except Exception:
+    _VecEnvBase = object
+
 SLOTS = 25
 
 
@@ -35,7 +47,7 @@ def _stream_handle(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-class SmartNanogridVecEnv:
+class SmartNanogridVecEnv(_VecEnvBase):
     """num_envs parallel SmartNanogridEnv-v0 environments on one GPU.
 
     Parameters (besides the reference's own keyword arguments):
@@ -49,6 +61,7 @@ class SmartNanogridVecEnv:
 
     metadata = {"render_modes": []}
     render_mode = None
+    render_modes = ()   # what SB3's VecEnv.__init__ reads through get_attr("render_modes")
 
     def __init__(self, num_envs=1, *, seed=0, device=0, rng="reference", info=False, env_offset=0, **env_kwargs):
         if torch is None or not torch.cuda.is_available():
@@ -98,6 +111,14 @@ class SmartNanogridVecEnv:
         self._warned_breakpoint = False
         self._last_reset = None   # 'generated', 'replay' or 'injected': how the loaded day began
         self.closed = False
+        # SB3 2.x VecEnv state: the reset infos (the reference's reset returns {}, :351), and the seeds /
+        # options that seed() / set_options() leave for the next reset
+        self.reset_infos = [{} for _ in range(E)]
+        self._seeds = [None] * E
+        self._options = [{} for _ in range(E)]
+        if _VecEnvBase is not object:   # pragma: no cover - SB3 is not in the image
+            _VecEnvBase.__init__(self, E, self.observation_space, self.action_space)
+            self.render_mode = None
 
     # ------------------------------------------------------------------ lifecycle
     def close(self):
@@ -145,8 +166,13 @@ class SmartNanogridVecEnv:
 
     # ------------------------------------------------------------------ device-resident API
     def reset_tensors(self, rng=None):
-        """New day for every env; returns the t=0 observations (device tensor [E, obs_dim])."""
+        """New day for every env; returns the t=0 observations (device tensor [E, obs_dim]).  A seed left by
+        seed() takes effect here."""
         self._check_mode()
+        self._apply_pending_seed()
+        return self._new_day(rng)
+
+    def _new_day(self, rng=None):
         mode = self.rng_mode if rng is None else (_native.RNG_DEVICE if rng == "device" else _native.RNG_REFERENCE)
         with torch.cuda.device(self.device):
             self.return_d.zero_()
@@ -165,6 +191,7 @@ class SmartNanogridVecEnv:
         observations (device tensor).  The reference's file is one per process; here each env replays its
         own last generated day."""
         self._check_mode()
+        self._apply_pending_seed()
         with torch.cuda.device(self.device):
             self.return_d.zero_()
             check(lib().sng_reset_replay(self._h, ctypes.c_void_p(self.obs_d.data_ptr()),
@@ -232,7 +259,8 @@ class SmartNanogridVecEnv:
         slots = 25, or T+1 with the build-defined extended day).  pv_ratio None: drawn per env from its
         Python stream."""
         self._check_mode()
-        arrs = [np.ascontiguousarray(a, np.float64) for a in (soc, occupancy, capacity, requested_soc)]
+        self._apply_pending_seed()
+        arrs =[np.ascontiguousarray(a, np.float64) for a in (soc, occupancy, capacity, requested_soc)]
         ai = np.ascontiguousarray(arrivals, np.int32)
         di = np.ascontiguousarray(departures, np.int32)
         sc = _native.SngScenario()
@@ -257,10 +285,31 @@ class SmartNanogridVecEnv:
         return self._obs_to_host()
 
     # ------------------------------------------------------------------ SB3 VecEnv API
+    _RESET_OPTIONS = ("generate_new_initial_values", "algorithm_used", "environment_mode", "initial_values",
+                      "pv_ratio", "restore_requested_soc")
+
     def reset(self, generate_new_initial_values=True, algorithm_used="", environment_mode="", **kwargs):
         """smart_nanogrid_environment.py:311-351.  generate_new_initial_values=False replays the last
         generated day (replay_tensors); with initial_values=<dict or list> (and optionally pv_ratio=,
-        restore_requested_soc=) it starts from those days instead (reset_from_initial_values)."""
+        restore_requested_soc=) it starts from those days instead (reset_from_initial_values).
+
+        SB3 2.x: the seeds of seed() and the options of set_options() apply here, then are cleared
+        (DummyVecEnv.reset).  The options are this method's keyword arguments; every env of the batch
+        resets alike, so per-env options must all be equal."""
+        opts = self._options
+        self._options = [{} for _ in range(self.num_envs)]
+        if any(opts):
+            if any(o != opts[0] for o in opts):
+                raise ValueError("set_options: every env of the batch resets alike; give one options dict")
+            unknown = set(opts[0]) - set(self._RESET_OPTIONS)
+            if unknown:
+                raise ValueError(f"set_options: unknown reset options {sorted(unknown)}")
+            o = dict(opts[0])
+            generate_new_initial_values = o.pop("generate_new_initial_values", generate_new_initial_values)
+            algorithm_used = o.pop("algorithm_used", algorithm_used)
+            environment_mode = o.pop("environment_mode", environment_mode)
+            kwargs = {**o, **kwargs}
+        self.reset_infos = [{} for _ in range(self.num_envs)]
         if algorithm_used:
             self.settings.algorithm_used = algorithm_used
         if environment_mode:
@@ -305,7 +354,12 @@ class SmartNanogridVecEnv:
             for i in range(E):
                 infos[i]["terminal_observation"] = obs[i]
                 infos[i]["TimeLimit.truncated"] = False
-            obs = self.reset()
+            # DummyVecEnv's automatic reset: a new day; seeds and options left by seed() / set_options()
+            # wait for the caller's next reset()
+            self._check_mode()
+            self._new_day()
+            self.reset_infos = [{} for _ in range(E)]
+            obs = self._obs_to_host()
         return obs, rewards, dones, infos
 
     def step(self, actions):
@@ -313,17 +367,36 @@ class SmartNanogridVecEnv:
         return self.step_wait()
 
     def seed(self, seed=None):
-        """SB3 VecEnv.seed: env i draws the streams of seed + i from the next reset on (reference RNG: what
+        """SB3 2.x VecEnv.seed: env i draws the streams of seed + i from the next reset on (reference RNG: what
         np.random.seed(seed + i); random.seed(seed + i) gives the reference; device RNG: the hash streams of
-        that seed from its first day).  seed=None picks a fresh seed.  The reference's own seed() is a no-op
-        (smart_nanogrid_environment.py:362-365) and it seeds through the global RNGs instead."""
+        that seed from its first day).  seed=None picks a fresh seed.  Returns the per-env seeds.  The
+        reference's own seed() is a no-op (smart_nanogrid_environment.py:362-365) and it seeds through the
+        global RNGs instead."""
         if seed is None:
-            seed = int(np.random.SeedSequence().entropy % (2 ** 31))
+            seed = int(np.random.randint(0, np.iinfo(np.uint32).max, dtype=np.uint32))
         seed = int(seed)
+        self._seeds = [seed + i for i in range(self.num_envs)]
+        return list(self._seeds)
+
+    def set_options(self, options=None):
+        """SB3 2.x VecEnv.set_options: keyword arguments of the next reset() (one dict for every env, or a
+        list of num_envs equal dicts)."""
+        if options is None:
+            options = {}
+        opts = ([dict(options) for _ in range(self.num_envs)] if isinstance(options, dict)
+                else [dict(o) for o in options])
+        if len(opts) != self.num_envs:
+            raise ValueError("set_options: need one options dict per env")
+        self._options = opts
+
+    def _apply_pending_seed(self):
+        if self._seeds[0] is None:
+            return
+        seed = self._seeds[0]
         with torch.cuda.device(self.device):
             check(lib().sng_set_seed(self._h, seed, _stream_handle(self.device)), self._h)
         self._seed = seed
-        return [seed + i for i in range(self.num_envs)]
+        self._seeds = [None] * self.num_envs
 
     def render(self, mode="human"):
         return None

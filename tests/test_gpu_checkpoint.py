@@ -80,3 +80,29 @@ def test_state_refuses_other_configuration():
         a.load_state(blob[:100])
     c.close()
     a.close()
+
+
+def test_state_refuses_inconsistent_headers():
+    """the header's section flags and size are checked against each other before any section
+    is read (a corrupt blob must not drive reads past its end); the configuration fingerprint hashes the
+    fields, so -0.0 and 0.0 are one configuration."""
+    import struct
+    E = 256
+    kw = dict(number_of_chargers=10, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+    a = SmartNanogridVecEnv(E, seed=1, rng="reference", grid_cost_weight=0.0, **kw)
+    a.reset_tensors()
+    blob = a.save_state()
+    total = struct.unpack_from("<Q", blob, 136)[0]
+    assert total == len(blob)
+    # StateHeader offsets: packed 72, has_word 112, has_req 116, has_prof 120, has_streams 128, total_bytes 136
+    for off, fmt, val in [(112, "<i", 0), (128, "<i", 0), (120, "<i", 1), (72, "<i", 1), (116, "<i", 7),
+                          (136, "<Q", total - 4 * 2 * 625 * E), (136, "<Q", 0)]:
+        bad = bytearray(blob)
+        struct.pack_into(fmt, bad, off, val)
+        with pytest.raises(NativeError, match="corrupt state header"):
+            a.load_state(bytes(bad))
+    b = SmartNanogridVecEnv(E, seed=2, rng="reference", grid_cost_weight=-0.0, **kw)
+    b.load_state(blob)
+    assert torch.equal(a.replay_tensors(), b.replay_tensors())
+    a.close()
+    b.close()

@@ -194,3 +194,29 @@ def test_replay_misuse_and_graph_encodings():
         v.replay_tensors()
     for x in (g_dev, g_rep, v, w):
         x.close()
+
+
+def test_unstepped_device_day_replayed_is_counted_once():
+    """a device day replayed before any of its steps was never counted (its first step counts
+    it, a replay's steps do not); the next device reset must still draw a new day -- the day a twin that
+    stepped the generated day draws next."""
+    E, N = 512, 10
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    v = SmartNanogridVecEnv(E, seed=21, rng="device", **kw)
+    twin = SmartNanogridVecEnv(E, seed=21, rng="device", **kw)
+    v.reset_tensors()
+    twin.reset_tensors()
+    day0 = v.get_scenarios()[0]
+    assert v.day_counter() == 0
+    v.replay_tensors()
+    for t in range(24):
+        v.step_tensors(acts[t])
+        twin.step_tensors(acts[t])
+    assert v.day_counter() == 1 == twin.day_counter()
+    v.reset_tensors()
+    twin.reset_tensors()
+    day1 = v.get_scenarios()[0]
+    assert day1 != day0 and day1 == twin.get_scenarios()[0]
+    v.close()
+    twin.close()

@@ -46,6 +46,49 @@ def test_seed_reseeds_the_streams(rng):
     b.close()
 
 
+def test_sb3_vecenv_contract():
+    """With SB3 importable (here: its abstract VecEnv stood in, tests/sb3_stub.py) the class is an SB3
+    VecEnv, and seed() / set_options() apply at the next reset() and not at the automatic reset after a
+    day, as DummyVecEnv does (SB3 2.x).  The days are those of the duck-typed class driven alike."""
+    from sb3_stub import VecEnv, load_vec_env_with_sb3
+    cls = load_vec_env_with_sb3().SmartNanogridVecEnv
+    E = 64
+    v = cls(E, seed=3, **KW)
+    ref = SmartNanogridVecEnv(E, seed=50, **KW)
+    assert isinstance(v, VecEnv) and v.reset_infos == [{}] * E and v.metadata == {"render_modes": ()}
+    assert v.seed(50) == [50 + i for i in range(E)]
+    np.testing.assert_array_equal(v.reset(), ref.reset())
+    rng = np.random.default_rng(5)
+    for t in range(24):
+        if t == 23:
+            v.seed(99)          # pending: the automatic reset below must not use it
+        a = rng.uniform(0, 1, (E, 11)).astype(np.float32)
+        o, r, d, info = v.step(a)
+        o_ref, r_ref, d_ref, info_ref = ref.step(a)
+        np.testing.assert_array_equal(o, o_ref)
+        np.testing.assert_array_equal(r, r_ref)
+        np.testing.assert_array_equal(d, d_ref)
+    assert d.all() and all("terminal_observation" in i for i in info)
+    np.testing.assert_array_equal(info[7]["terminal_observation"], info_ref[7]["terminal_observation"])
+    # the pending seed 99 applies at this reset: the day of a fresh population seeded 99
+    fresh = SmartNanogridVecEnv(E, seed=99, **KW)
+    np.testing.assert_array_equal(v.reset()[:, :-1], fresh.reset()[:, :-1])   # BESS carries v's history
+    assert v.get_scenarios()[0] == fresh.get_scenarios()[0]
+    # options: the next reset() replays the day (generate_new_initial_values=False), then they are cleared
+    v.set_options({"generate_new_initial_values": False})
+    fresh.set_options({"generate_new_initial_values": False})
+    day = v.get_scenarios()[0]
+    v.reset()
+    fresh.reset()
+    np.testing.assert_array_equal(v.pv_ratio(), fresh.pv_ratio())
+    assert [d["Arrivals"] for d in v.get_scenarios()[0]] == [d["Arrivals"] for d in day]
+    assert v._options == [{}] * E and v.reset_infos == [{}] * E
+    v.reset()
+    assert v.get_scenarios()[0] != day
+    for x in (v, ref, fresh):
+        x.close()
+
+
 def test_attributes_and_methods_per_index():
     E = 8
     v = SmartNanogridVecEnv(E, seed=4, **KW)
@@ -173,4 +216,48 @@ def test_steps_only_graph_refuses_other_encodings():
     with pytest.raises(NativeError, match="t = 0"):
         g.launch()
     g.close()
+    v.close()
+
+
+def test_graphs_refuse_a_changed_seed():
+    """a captured graph's kernels carry the seed and env offset by value; after seed() (or a
+    restored state) has changed them, launching it would replay the old streams' days, so it refuses."""
+    E, N = 512, 10
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    v = SmartNanogridVecEnv(E, seed=4, rng="device", **KW)
+    g = EpisodeGraph(v, acts, with_reset=True)
+    g.launch()
+    v.reset_tensors()
+    s = EpisodeGraph(v, acts, with_reset=False)
+    v.seed(5)
+    v.reset_tensors()               # the seed applies here
+    for gr in (g, s):
+        with pytest.raises(NativeError, match="recapture"):
+            gr.launch()
+    g2 = EpisodeGraph(v, acts, with_reset=True)   # recaptured: the new seed's days
+    g2.launch()
+    for x in (g, s, g2, v):
+        x.close()
+
+
+def test_failed_injection_invalidates_the_day():
+    """days are uploaded chunk by chunk as they are encoded; when a later env's day is
+    refused, the earlier chunks have already overwritten the loaded day, so step / replay refuse until
+    the next reset instead of stepping a half-replaced day."""
+    E = 4096
+    v = SmartNanogridVecEnv(E, seed=12, rng="reference", **KW)
+    v.reset_tensors()
+    iv, r = v.get_scenarios()
+    bad = iv[-1]
+    c = next(c for c in range(10) if any(bad["Charger_occupancy"][c]))
+    t = bad["Charger_occupancy"][c].index(1.0)
+    bad["Vehicle_capacities"][c][t] = 0.0          # an occupied slot with no battery: refused
+    with pytest.raises(NativeError, match="reset again"):
+        v.reset_from_initial_values(iv, r)
+    with pytest.raises(NativeError, match="before reset"):
+        v.step_tensors(torch.zeros((E, 11), device="cuda:0"))
+    with pytest.raises(NativeError):
+        v.replay_tensors()
+    v.reset_tensors()
+    v.step_tensors(torch.zeros((E, 11), device="cuda:0"))
     v.close()
