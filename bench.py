@@ -9,6 +9,7 @@ action Box, 20 % exact zeros), pre-generated on the device outside the timed reg
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--chargers C] [--no-cpu-baseline]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+        [--dist-backend gloo]   # several ranks on one GPU: day returns gathered through host memory
 
 Rank 0 prints one JSON line.  `roofline` describes the dominant kernel (the fused step):
 achieved = SURVEY.md 8(d)'s algorithmic bytes per env-step, B(N) = 40 N + 65 (465 B at N = 10),
@@ -18,13 +19,16 @@ start-to-start time rocprofv3 reports for a graph's kernels.  The reset kernel's
 dispatch time of the step kernel (`eager_launch_us`, `frac_eager`) come from HIP start/stop events
 attached to every dispatch of eager days right after the timed region, on the stream the kernels run on.
 `frac_rocprof` is the same bytes over the average duration of that kernel in the committed
-rocprofv3 --kernel-trace --stats summary (profiles/), when one exists for this kernel;
-`measured_copy_gbs` is this GPU's device-to-device copy bandwidth (1 GiB, read + write bytes), the
-measured ceiling SURVEY.md 8(d) asks to quote beside the 8 TB/s spec; `traffic` is
-the HBM bytes per launch from the committed PMC passes, null if absent.  `cpu_baseline` is the C
-restatement of the reference's step()/reset() (oracle/, kind "port", label "restatement") run as one
-process per host core of sched_getaffinity (capped by OMP_NUM_THREADS), measured before the GPU is
-touched, with the reference's own Python step() range from SURVEY.md section 6 beside it.
+rocprofv3 --kernel-trace --stats summary (profiles/), when one exists for this kernel.  Beside the
+SURVEY.md 8(d) fraction: `frac_layout` prices the bytes this layout actually moves (32N + 89 B per env-step,
++4 B for the error flags the default SngInfo writes), `frac_pmc` the PMC-measured HBM bytes (`traffic`,
+from the committed passes, null if absent), and `copy_step_size` / `copy_1gib` are the measured ceiling
+SURVEY.md 8(d) asks for: libsng's float4 copy probe (sng_bandwidth_probe) moving the step's own read and
+write bytes in one dispatch, and 1 GiB.  The step is timed with the default SngInfo (flag store on;
+--no-flags times it without).  `cpu_baseline` is the C restatement of the reference's step()/reset()
+(oracle/, kind "port", label "restatement") run as one process per host core granted by the cgroup CPU
+quota (sched_getaffinity shows the whole machine on a GPU box), measured before the GPU is touched, with
+the reference's own Python step() range from SURVEY.md section 6 beside it.
 """
 import argparse
 import glob
@@ -52,13 +56,16 @@ def survey_bytes(n):
     return 40 * n + 65
 
 
-def step_kernel_bytes(n, noise=False):
-    """What this layout moves per env-step of a device-RNG day (b-pv, no requested-SoC stream): actions
-    4(N+1) + obs 4(2N+9) + reward 8 + done 1 + EV SoC r/w 16N + packed 4-byte charger-step record 4N
-    (sng_layout.h) + BESS r/w 16 + PV ratio 8 + day-return r/w 16 = 32N + 89 (+ 64 for the PV / price
-    profile factors of t..t+3 with stochastic profiles).  Host-RNG days read the word and a float64
-    static SoC instead: 40N + 89."""
-    return 4 * (n + 1) + 4 * (2 * n + 9) + 8 + 1 + 16 * n + 4 * n + 16 + 8 + 16 + (64 if noise else 0)
+def step_kernel_bytes(n, noise=False, flags=True):
+    """What this layout moves per env-step of a device-RNG day (b-pv, no requested-SoC stream), as
+    (read, written): reads = actions 4(N+1) + packed 4-byte charger-step record 4N (sng_layout.h) + EV SoC
+    8N + BESS 8 + PV ratio 8 + day return 8 (+ 64 for the PV / price profile factors of t..t+3 with
+    stochastic profiles); writes = obs 4(2N+9) + reward 8 + done 1 + EV SoC 8N + BESS 8 + day return 8
+    (+ 4 for the per-env error flags the default SngInfo passes).  32N + 89 (+4) in all.  Host-RNG days
+    read the word and a float64 static SoC instead: 40N + 89."""
+    rd = 4 * (n + 1) + 4 * n + 8 * n + 8 + 8 + 8 + (64 if noise else 0)
+    wr = 4 * (2 * n + 9) + 8 + 1 + 8 * n + 8 + 8 + (4 if flags else 0)
+    return rd, wr
 
 
 def _cpu_worker(job):
@@ -79,13 +86,49 @@ def _cpu_worker(job):
     return envs * cfg.T, time.perf_counter() - t0
 
 
+def cgroup_cpus():
+    """The CPU share the cgroup grants this process: cpu.max (cgroup v2) or cfs_quota_us / cfs_period_us
+    (v1) as (cores, text); (None, text) when there is no quota."""
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", None)):
+        try:
+            with open(path) as fp:
+                txt = fp.read().strip()
+        except OSError:
+            continue
+        if parse is not None:
+            quota, period = parse(txt)[:2]
+        else:
+            try:
+                with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fp:
+                    period = fp.read().strip()
+            except OSError:
+                return None, f"{path}={txt}"
+            quota = txt
+        src = f"{path}={txt}" + ("" if parse is not None else f"/{period}")
+        if quota in ("max", "-1"):
+            return None, src
+        return max(1, int(int(quota) // int(period))), src
+    return None, "no cgroup cpu quota file"
+
+
 def cpu_baseline(kw, budget_s):
-    """The restatement on every host core this process may use (sched_getaffinity, capped by
-    OMP_NUM_THREADS / SNG_CPU_BASELINE_PROCS: a GPU box shows the whole machine but gives a process a
-    share), one process per core, forked before the GPU is initialised."""
+    """The restatement on every host core this process is granted, one process per core, forked before
+    the GPU is initialised: the cgroup CPU quota (a GPU box shows the whole machine in sched_getaffinity
+    but grants a share of it), else sched_getaffinity capped by OMP_NUM_THREADS; SNG_CPU_BASELINE_PROCS
+    overrides both."""
     affinity = len(os.sched_getaffinity(0))
-    cap = os.environ.get("SNG_CPU_BASELINE_PROCS") or os.environ.get("OMP_NUM_THREADS")
-    procs = max(1, min(affinity, int(cap))) if cap else affinity
+    quota, quota_src = cgroup_cpus()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    forced = os.environ.get("SNG_CPU_BASELINE_PROCS")
+    if forced:
+        procs, cap = max(1, int(forced)), f"SNG_CPU_BASELINE_PROCS={forced}"
+    elif quota is not None:
+        procs, cap = min(affinity, quota), f"cgroup quota {quota} CPUs ({quota_src})"
+    elif omp:
+        procs, cap = max(1, min(affinity, int(omp))), f"no cgroup quota ({quota_src}); OMP_NUM_THREADS={omp}"
+    else:
+        procs, cap = affinity, f"no cgroup quota ({quota_src})"
     import oracle as O
     O.lib()   # build / load once in the parent: the forked workers inherit it
     with multiprocessing.get_context("fork").Pool(procs) as pool:
@@ -98,7 +141,8 @@ def cpu_baseline(kw, budget_s):
             "per_process": float(np.mean(per)),
             "sample": f"{steps // T} envs x 1 day (reset + {T} steps each), b-pv N={kw['number_of_chargers']} sparse "
                       f"{kw.get('time_interval', '1h')}; C restatement of the reference (oracle/), {procs} processes "
-                      f"(sched_getaffinity {affinity} CPUs, cap {cap or 'none'}), {wall:.1f} s",
+                      f"(sched_getaffinity {affinity} CPUs; {cap}), {wall:.1f} s",
+            "cores_source": cap,
             "reference_python": {"value": [4700, 8200], "unit": "env-steps/s per core",
                                  "source": "SURVEY.md section 6: the reference's own step()+reset(), N=10, JSON I/O "
                                            "stubbed, in the build container (the reference does not exist on the "
@@ -136,26 +180,21 @@ def load_pmc_traffic(n_envs, chargers, kernel):
     return None
 
 
-def measured_copy_gbs(device, mib=1024, reps=5):
-    """Device-to-device copy bandwidth on this GPU (read + write bytes / time), the measured ceiling the
-    roofline is also quoted against: torch's copy kernel over two 1 GiB buffers, HIP events,
-    best of `reps`."""
-    n = mib * (1 << 20) // 4
-    a = torch.empty(n, dtype=torch.float32, device=device).fill_(1.0)
-    b = torch.empty_like(a)
-    b.copy_(a)
-    best = None
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        b.copy_(a)
-        e1.record()
-        torch.cuda.synchronize()
-        ms = e0.elapsed_time(e1)
-        best = ms if best is None else min(best, ms)
-    del a, b
-    torch.cuda.empty_cache()
-    return 2 * n * 4 / (best * 1e-3) / 1e9
+def copy_ceiling(device, read_bytes, write_bytes, reps=50):
+    """The measured bandwidth ceiling SURVEY.md 8(d) asks to quote beside the 8 TB/s spec: libsng's float4
+    copy probe (sng_bandwidth_probe: one float4 per thread, nontemporal stores like the step) moving
+    read_bytes + write_bytes per dispatch.  Returns GB/s for the dispatch's own device time (start/stop
+    events per dispatch) and for back-to-back dispatches (start to start, as the day graphs run the step)."""
+    import ctypes
+    from smart_nanogrid_gym._native import check, lib
+    d_us, b_us = ctypes.c_float(), ctypes.c_float()
+    check(lib().sng_bandwidth_probe(device.index or 0, int(read_bytes), int(write_bytes), int(reps),
+                                    ctypes.byref(d_us), ctypes.byref(b_us),
+                                    ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)))
+    tot = read_bytes + write_bytes
+    return {"read_bytes": int(read_bytes), "write_bytes": int(write_bytes), "dispatch_us": round(d_us.value, 3),
+            "back_to_back_us": round(b_us.value, 3), "gbs_dispatch": round(tot / (d_us.value * 1e-6) / 1e9, 1),
+            "gbs_back_to_back": round(tot / (b_us.value * 1e-6) / 1e9, 1)}
 
 
 def main():
@@ -175,6 +214,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--timing-days", type=int, default=3, help="eager days for the per-kernel HIP-event probe")
     ap.add_argument("--graph-days", type=int, default=20, help="days per graph replay (divides steps)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: RCCL over xGMI (default), or gloo with the day returns staged through host "
+                         "memory (several ranks on one GPU, tests)")
+    ap.add_argument("--no-flags", action="store_true",
+                    help="time the step without the per-env error-flag store (the default SngInfo keeps it)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,18 +235,26 @@ def main():
     # workers, host cores otherwise idle)
     cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(kw, args.cpu_budget)
     dist = None
+    # one GPU per rank; ranks beyond the visible GPUs share them (gloo only: RCCL needs one rank per GPU).
+    # torch.cuda.device_count() does not initialise the GPU on this image.
+    ndev = max(1, torch.cuda.device_count())
+    gpu = local % ndev
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    device = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
+    coll_dev = device if args.dist_backend == "nccl" else None   # where the collectives' tensors live
 
     from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv
     from smart_nanogrid_gym.parallel import DayReturnExchange, max_over_ranks, shard_envs
 
     offset, _ = shard_envs(world * E, world, rank)   # weak scaling: E envs per GPU, global ids
-    venv = SmartNanogridVecEnv(E, seed=args.seed, device=local, rng="device", env_offset=offset,
+    venv = SmartNanogridVecEnv(E, seed=args.seed, device=gpu, rng="device", env_offset=offset,
                                step_lanes_per_env=args.lanes, **kw)
     T, A = venv.timesteps, venv.act_dim
     g = torch.Generator(device=device).manual_seed(args.seed + rank)
@@ -211,8 +263,9 @@ def main():
     acts = low + (high - low) * torch.rand((T, E, A), generator=g, device=device)
     acts = torch.where(torch.rand(acts.shape, generator=g, device=device) < 0.2, torch.zeros_like(acts), acts)
     acts = acts.contiguous()
-    # the bench's info: only the per-env day return (for the all-gather), no diagnostics
-    venv._info.flags = None
+    # the default SngInfo: the per-env error flags and the day return (for the all-gather), no diagnostics
+    if args.no_flags:
+        venv._info.flags = None
     venv.reset_tensors(rng="device")
     kernel = venv.step_kernel_name()   # the instantiation the graphs below launch (device-RNG days)
     # days per graph replay (the same at every N, so per-GPU work is identical)
@@ -224,7 +277,7 @@ def main():
         # N > 1: every day's per-env returns land in a [D, E] snapshot (one per graph, two
         # alternating graphs) and one RCCL all-gather per replay runs on the collective stream
         # while the next replay computes
-        xch = DayReturnExchange(D, E, device)
+        xch = DayReturnExchange(D, E, device, staging="device" if args.dist_backend == "nccl" else "host")
         graphs = [EpisodeGraph(venv, acts, with_reset=True, days=D, day_returns=xch.snap[k]) for k in range(2)]
     else:
         graphs = [EpisodeGraph(venv, acts, with_reset=True, days=D)]
@@ -274,7 +327,7 @@ def main():
                   f"{reset_us:.2f} us) / {T} step dispatches; reset and eager_launch_us from HIP start/stop "
                   f"events on each dispatch (hipExtLaunchKernel), {args.timing_days} eager days after the "
                   f"timed region, same stream/env/actions")
-    elapsed = max_over_ranks(elapsed, device=device)
+    elapsed = max_over_ranks(elapsed, device=coll_dev)
     # sanity: a day's returns are finite and <= 0
     ret = venv.return_d.cpu().numpy()
     assert np.isfinite(ret).all() and (ret <= 0).all()
@@ -287,20 +340,37 @@ def main():
         env_steps = world * E * T * args.steps
         value = env_steps / elapsed
         launch_s = graph_step_us * 1e-6
+        eager_s = float(np.mean(kernel_ms)) * 1e-3
         bpl = survey_bytes(N) * E
         achieved = bpl / launch_s / 1e9
+        rd, wr = step_kernel_bytes(N, noise, flags=not args.no_flags)
+        lpl = (rd + wr) * E
+        traffic = load_pmc_traffic(E, N, kernel)
         rp_us, rp_file = rocprof_average_us(kernel, args.extended_day or noise)
-        copy_gbs = measured_copy_gbs(device)
+        # measured ceilings: the same copy kernel at this step's own read/write bytes (one dispatch) and at
+        # 1 GiB (512 MiB each way)
+        c_step = copy_ceiling(device, rd * E, wr * E)
+        c_big = copy_ceiling(device, 1 << 29, 1 << 29, reps=10)
+        frac = lambda b, sec: round(b / sec / 1e9 / HBM_PEAK_GBS, 4)   # noqa: E731
         roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_pmc_traffic(E, N, kernel),
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "kernel": kernel, "bytes_model": f"SURVEY.md 8(d) B(N) = 40N+65 = {survey_bytes(N)} B per env-step",
-                "bytes_per_launch": bpl, "layout_bytes_per_launch": step_kernel_bytes(N, noise) * E,
+                "bytes_per_launch": bpl,
+                "layout_bytes_model": f"this layout: {rd} B read + {wr} B written per env-step "
+                                      f"(bench.step_kernel_bytes; flag store {'off' if args.no_flags else 'on'})",
+                "layout_bytes_per_launch": lpl,
+                "frac_layout": frac(lpl, launch_s),
+                "frac_pmc": None if traffic is None else frac(traffic, launch_s),
+                "traffic_source": "profiles/pmc_step_kernel.json (rocprofv3 FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)",
                 "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src,
-                "eager_launch_us": round(float(np.mean(kernel_ms)) * 1e3, 3), "reset_us": round(reset_us, 3),
-                "frac_eager": round(bpl / (float(np.mean(kernel_ms)) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "measured_copy_gbs": round(copy_gbs, 1), "frac_of_measured_copy": round(achieved / copy_gbs, 4),
+                "eager_launch_us": round(eager_s * 1e6, 3), "reset_us": round(reset_us, 3),
+                "frac_eager": frac(bpl, eager_s), "frac_layout_eager": frac(lpl, eager_s),
+                "copy_step_size": c_step, "copy_1gib": c_big,
+                "frac_of_copy_step_size": round(lpl / launch_s / 1e9 / c_step["gbs_back_to_back"], 4),
+                "frac_of_copy_step_size_eager": round(lpl / eager_s / 1e9 / c_step["gbs_dispatch"], 4),
                 "rocprof_avg_us": rp_us, "rocprof_file": rp_file,
-                "frac_rocprof": None if rp_us is None else round(bpl / (rp_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+                "frac_rocprof": None if rp_us is None else frac(bpl, rp_us * 1e-6),
+                "frac_layout_rocprof": None if rp_us is None else frac(lpl, rp_us * 1e-6)}
         headline = (N == 10 and T == 24 and not noise)
         metric = METRIC if headline else f"env-steps/sec (whole node) at N={E:,} envs × {N} chargers, {T}-step day"
         desc = f"b-pv bounded sparse {args.time_interval}" + (
@@ -314,7 +384,10 @@ def main():
                           "step_unit": "one simulated day of every env",
                           "days_per_graph_replay": D,
                           "parallelism": f"env-sharded x{world}" + (
-                              ", RCCL all-gather of every day's returns, one per replay, overlapped" if world > 1 else "")},
+                              (", RCCL all-gather of every day's returns, one per replay, overlapped"
+                               if args.dist_backend == "nccl" else
+                               ", gloo all-gather of every day's returns staged through host memory, one per replay")
+                              if world > 1 else "")},
                "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out))
     for gr in graphs:

@@ -309,6 +309,14 @@ int32_t sng_host_threads(void);
  * reset draws day *out).  Synchronises `stream`. */
 int sng_get_day_counter(SngEnv *env, uint64_t *out, void *stream);
 
+/* Diagnostics: the measured bandwidth ceiling of device `device` for a step-sized launch.  One float4
+ * copy kernel reads read_bytes and writes write_bytes (nontemporal stores, the step kernel's policy) per
+ * dispatch; *dispatch_us = mean device time of `reps` dispatches each between its own start/stop events,
+ * *back_to_back_us = mean start-to-start time of `reps` dispatches queued back to back (as a graph runs
+ * them).  Allocates and frees its buffers; synchronises `stream`.  No reference counterpart. */
+int sng_bandwidth_probe(int device, int64_t read_bytes, int64_t write_bytes, int32_t reps, float *dispatch_us,
+                        float *back_to_back_us, void *stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Multi-GPU exchange: one process per GPU, each with its contiguous env shard
  * (sng_set_env_offset); once per simulated day the per-env returns are all-gathered over RCCL

@@ -37,6 +37,8 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
                            hipStream_t stream, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hipStream_t stream);
 hipError_t launch_bump_day(const DeviceState &s, hipStream_t stream);
+hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, hipStream_t stream, hipEvent_t a,
+                             hipEvent_t b);
 hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream);
 hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
                           int i1, hipStream_t stream);
@@ -1773,6 +1775,45 @@ int sng_time_step_kernels(SngEnv *env, const float *actions, float *obs, double 
     env->gen_loaded = true;
     env->t = T;
     env->day_finished = true;
+    return SNG_OK;
+}
+
+int sng_bandwidth_probe(int device, int64_t read_bytes, int64_t write_bytes, int32_t reps, float *dispatch_us,
+                        float *back_to_back_us, void *stream) {
+    if (read_bytes < 0 || write_bytes < 0 || read_bytes + write_bytes < 16 || reps < 1)
+        return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "sng_bandwidth_probe: bad sizes");
+    if (hipSetDevice(device) != hipSuccess) return fail(nullptr, SNG_ERR_HIP, "sng_bandwidth_probe: hipSetDevice");
+    hipStream_t st = as_stream(stream);
+    const int64_t nr = read_bytes / 16, nw = write_bytes / 16;
+    void *in = nullptr, *out = nullptr;
+    std::vector<hipEvent_t> ev(2 * (size_t)reps + 2, nullptr);
+    hipError_t e = hipMalloc(&in, (size_t)std::max<int64_t>(nr, 1) * 16);
+    if (e == hipSuccess) e = hipMalloc(&out, (size_t)std::max<int64_t>(nw, 1) * 16);
+    if (e == hipSuccess) e = hipMemsetAsync(in, 0, (size_t)std::max<int64_t>(nr, 1) * 16, st);
+    for (auto &x : ev)
+        if (e == hipSuccess) e = hipEventCreate(&x);
+    // warm-up, then `reps` dispatches each between its own start/stop events (the dispatch's device time),
+    // then `reps` back to back between two events (start to start, as a graph runs kernels)
+    for (int k = 0; e == hipSuccess && k < 3; ++k) e = launch_probe_copy(in, out, nr, nw, st, nullptr, nullptr);
+    for (int k = 0; e == hipSuccess && k < reps; ++k)
+        e = launch_probe_copy(in, out, nr, nw, st, ev[2 * (size_t)k], ev[2 * (size_t)k + 1]);
+    if (e == hipSuccess) e = hipEventRecord(ev[2 * (size_t)reps], st);
+    for (int k = 0; e == hipSuccess && k < reps; ++k) e = launch_probe_copy(in, out, nr, nw, st, nullptr, nullptr);
+    if (e == hipSuccess) e = hipEventRecord(ev[2 * (size_t)reps + 1], st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    float sum = 0.f, ms = 0.f;
+    for (int k = 0; e == hipSuccess && k < reps; ++k) {
+        e = hipEventElapsedTime(&ms, ev[2 * (size_t)k], ev[2 * (size_t)k + 1]);
+        sum += ms;
+    }
+    if (e == hipSuccess) e = hipEventElapsedTime(&ms, ev[2 * (size_t)reps], ev[2 * (size_t)reps + 1]);
+    for (auto x : ev)
+        if (x) (void)hipEventDestroy(x);
+    if (in) (void)hipFree(in);
+    if (out) (void)hipFree(out);
+    if (e != hipSuccess) return fail(nullptr, SNG_ERR_HIP, std::string("sng_bandwidth_probe: ") + hipGetErrorString(e));
+    if (dispatch_us) *dispatch_us = sum / reps * 1e3f;
+    if (back_to_back_us) *back_to_back_us = ms / reps * 1e3f;
     return SNG_OK;
 }
 

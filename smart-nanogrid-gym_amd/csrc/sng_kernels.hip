@@ -772,6 +772,193 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
 }
 
 // ---------------------------------------------------------------------------------
+// The wide lean step kernel: step_lean_kernel's recipe for stations wider than 16 chargers (BASELINE
+// config 5: N = 50, 15-minute steps, stochastic PV / price profiles), one wavefront per 64 envs, one
+// wavefront per workgroup, one wavefront per SIMD at E = 65,536 (so the whole 512-entry register file:
+// every charger's state is loaded up front).  What makes it lean at N = 50:
+//   - the charging total is the running sum whenever that equals numpy's pairwise sum of the compacted
+//     positive powers exactly (step_lean_kernel's argument: fewer than 8 terms, or float32 powers whose
+//     sum stays below 2^28 times the smallest), instead of numpy's 8-accumulator schedule fed one
+//     power at a time (PairwiseSum: ~40 VALU per power, two per charger);
+//   - the discharging total is exactly 0.0 (numpy's sum of an empty array) when no action of the wave is
+//     negative: a negative power needs a negative action (charger.py:37-56, 108-140), and then no power
+//     is positive other than a charging product.  A wavefront with a negative action (V2X) takes the
+//     general order, PairwiseSum over both signs, in a rolled loop that re-reads each charger's inputs
+//     (rare: nothing in the fast loop indexes the register arrays at run time);
+//   - a lane whose positive sum is not provably exact rebuilds its compacted positive powers from what
+//     the step leaves unchanged -- the records (occupancy) and the actions tile (the float32 product
+//     charger.py:92-94) -- and sums them in numpy's order (rare);
+//   - constants by value, one kernarg round trip before the loads, 1/cap by recip_cap, no LDS but the
+//     actions and observation tiles (40 KB per wavefront: four per CU).
+// ---------------------------------------------------------------------------------
+template <int NC>
+struct WideLds {
+    static constexpr int A = NC + 1;   // actions per env with a BESS (one fewer without)
+    static constexpr int O = 2 * NC + 9;
+    static constexpr int ACT = round4(kWave * A), OBS = round4(kWave * O);
+    static constexpr size_t BYTES = (size_t)(ACT + OBS) * 4;
+};
+
+// The NEP 50 float32 charging power of action a (charger.py:92-94), as charger_step computes it.
+__device__ __forceinline__ double charging_power(const Params &p, float a) {
+    return (double)__fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
+}
+
+template <int NC, bool PK, bool REQ, bool NOISE>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) void step_wide_kernel(
+    const float *__restrict__ act, float *__restrict__ obs, double *__restrict__ reward, uint8_t *__restrict__ done,
+    int64_t E, int t, int vec_io, StepConst k, Params p, DeviceState s, InfoPtrs info) {
+    using Lay = WideLds<NC>;
+    constexpr int KT = (Lay::A * kWave + 4 * kWave - 1) / (4 * kWave);
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int Ad = p.act_dim, O = p.obs_dim;
+    const int lane = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * kWave;   // the grid covers E exactly: every wave has an env
+    const int nw = (E - e0) < kWave ? (int)(E - e0) : kWave;
+    const bool live = lane < nw;
+    float *s_act = lds;
+    float *s_obs = lds + Lay::ACT;
+    const int64_t el = live ? e0 + lane : E - 1;   // idle lanes load a valid env and discard it
+    const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;
+    const size_t plane = (size_t)t * NC * (size_t)E;   // this step's timeline planes
+    const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
+
+    // loads oldest-needed-first: the actions tile and the per-env values, then every charger's state
+    TileStage<KT, kWave> act_tile;
+    act_tile.issue(act + e0 * Ad, nw * Ad, vec_io != 0, lane);
+    const double ratio = bld(s.ratio, el8);
+    const double bess_l = bld(p.bess ? s.bess : s.ratio, el8);
+    const double pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
+    const double ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
+    double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
+    if constexpr (NOISE) {   // the day's profile factors of t..t+3 (profile_kernel)
+        const size_t pp = (size_t)(p.T + 3) * E;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            fpv[j] = bld(s.prof + (size_t)(t + j) * E, el8);
+            fpr[j] = bld(s.prof + pp + (size_t)(t + j) * E, el8);
+        }
+    }
+    uint32_t w[NC];
+    double aux[PK ? 1 : NC], run[NC], req[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
+        if (PK) {
+            w[c] = bld(rec_t, el4, r4);
+        } else {
+            w[c] = bld(s.word + plane, el4, r4);
+            aux[PK ? 0 : c] = bld(s.aux + plane, el8, r8);
+        }
+        run[c] = bld(s.soc, el8, r8);
+        req[c] = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
+    }
+    act_tile.commit(s_act, lane);
+    wave_lds_fence();
+
+    const float *a_row = s_act + lane * Ad;
+    float *o_row = s_obs + lane * O;
+    float av[NC];
+    float amin = 0.0f;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+        av[c] = a_row[c];
+        amin = __builtin_fminf(amin, av[c]);   // a NaN action is not negative (fmin drops it)
+    }
+    const float bess_action = p.bess ? a_row[NC] : 0.0f;
+    const int k_soc = p.pv ? 8 : 4;
+    if (live) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, fpv, fpr);
+
+    double pen_v = 0.0, p_ch = 0.0, p_dis = 0.0;
+    uint32_t n_nonexist = 0, fl = 0;
+    if (__builtin_amdgcn_ballot_w64(live && amin < 0.0f) == 0) {
+        // the fast loop: no negative action in the wave, so no negative power (p_dis stays 0.0)
+        double seq_pos = 0.0, pmin = __builtin_inf();
+        int n_pos = 0;
+        if (live) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const uint32_t capi = (w[c] >> W_CAP_SHIFT) & 0xffu;
+                const bool occ = (w[c] & W_OCC) != 0;
+                const ChargerResult r = charger_step<true, true>(p, PK ? (w[c] & ~W_STATIC) : w[c],
+                                                                 PK ? 0.0 : aux[PK ? 0 : c], run[c], req[c], av[c], t,
+                                                                 recip_cap((double)capi));
+                bst<kNT>(s.soc, el8, (PK && !occ) ? (double)rec_soc(w[c]) : r.soc, (uint32_t)c * (uint32_t)E * 8u);
+                o_row[k_soc + c] = (float)r.soc;
+                o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[c]);
+                n_nonexist += r.nx;
+                fl |= r.fl;
+                pen_v += r.q;
+                const bool ip = r.pw > 0.0;
+                seq_pos += __builtin_fmax(r.pw, 0.0);
+                n_pos += ip ? 1 : 0;
+                pmin = __builtin_fmin(pmin, ip ? r.pw : __builtin_inf());
+                __builtin_amdgcn_sched_barrier(0);   // charger c waits only for its own loads
+            }
+        }
+        p_ch = seq_pos;
+        const bool pos_slow = live && n_pos >= 8 && !(seq_pos <= pmin * 0x1.0p28);
+        if (__builtin_amdgcn_ballot_w64(pos_slow)) {   // wave-uniform: rare
+            if (pos_slow) {
+                // the compacted positive powers again, in charger order: an occupied charger charging with
+                // a > 0 under bounded charging bills pc (charger.py:58-94); nothing else is positive here
+                PairwiseSum pos;
+                pos.init();
+#pragma unroll 1
+                for (int c = 0; c < NC; ++c) {
+                    const uint32_t wc = PK ? bld(rec_t, el4, (uint32_t)c * (uint32_t)E * 4u)
+                                           : bld(s.word + plane, el4, (uint32_t)c * (uint32_t)E * 4u);
+                    const float a = a_row[c];
+                    const double pc = charging_power(p, a);
+                    if ((wc & W_OCC) && p.bounded && a > 0.0f && pc > 0.0) pos.push(pc);
+                }
+                p_ch = pos.result();
+            }
+        }
+    } else {
+        // a wave with a discharging action: numpy's pairwise order for both signs (PairwiseSum), one
+        // charger at a time, its inputs re-read from memory and the actions tile
+        PairwiseSum pos, neg;
+        pos.init();
+        neg.init();
+        if (live) {
+#pragma unroll 1
+            for (int c = 0; c < NC; ++c) {
+                const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
+                const uint32_t wc = PK ? bld(rec_t, el4, r4) : bld(s.word + plane, el4, r4);
+                const double auxc = PK ? 0.0 : bld(s.aux + plane, el8, r8);
+                const double runc = bld(s.soc, el8, r8);
+                const double reqc = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
+                const uint32_t capi = (wc >> W_CAP_SHIFT) & 0xffu;
+                const bool occ = (wc & W_OCC) != 0;
+                const ChargerResult r = charger_step<true, true>(p, PK ? (wc & ~W_STATIC) : wc, auxc, runc, reqc,
+                                                                 a_row[c], t, recip_cap((double)capi));
+                bst<kNT>(s.soc, el8, (PK && !occ) ? (double)rec_soc(wc) : r.soc, r8);
+                o_row[k_soc + c] = (float)r.soc;
+                o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : wc);
+                n_nonexist += r.nx;
+                fl |= r.fl;
+                pen_v += r.q;
+                if (r.pw > 0.0) pos.push(r.pw);
+                if (r.pw < 0.0) neg.push(r.pw);
+            }
+        }
+        p_ch = pos.result();
+        p_dis = neg.result();
+    }
+    if (live) {
+        pen_v += (t == 0) ? pen0_l : 0.0;   // python index -1 slot; every per-charger term is 0 at t = 0
+        env_tail<false>(p, s, info, e0, (uint32_t)lane, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action, p_ch,
+                        p_dis, pen_v, 100.0 * (double)n_nonexist, fl, o_row, k.v, fpv, fpr,
+                        info.episode_return ? ret_l : 0.0, 0.0, reward, done);
+    }
+    wave_lds_fence();
+    copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
+    if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0)
+        __hip_atomic_fetch_add(s.episode, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ---------------------------------------------------------------------------------
 // The fused step: SmartNanogridEnv.step(actions) for BLOCK/L envs per workgroup.
 // NC   = compile-time charger count (0: runtime p.n, L must be 1);
 // L    = lanes per env;
@@ -1513,6 +1700,32 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
 }
 
 // ---------------------------------------------------------------------------------
+// Bandwidth probe (diagnostics, sng_bandwidth_probe): the measured ceiling the step kernel's roofline is
+// quoted against.  One float4 per thread: thread i reads in[i] when i < nr and writes out[i] when
+// i < nw (nontemporal, the step's store policy), so one dispatch moves 16 (nr + nw) bytes.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void probe_copy_kernel(const float4 *__restrict__ in, float4 *__restrict__ out,
+                                                         int64_t nr, int64_t nw) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    typedef float v4f __attribute__((ext_vector_type(4)));
+    v4f v = {0.f, 0.f, 0.f, 0.f};
+    if (i < nr) v = reinterpret_cast<const v4f *>(in)[i];
+    if (i < nw) __builtin_nontemporal_store(v, reinterpret_cast<v4f *>(out) + i);
+}
+
+hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, hipStream_t stream, hipEvent_t a,
+                             hipEvent_t b) {
+    const int64_t n = nr > nw ? nr : nw;
+    const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+    if (a && b)
+        hipExtLaunchKernelGGL(probe_copy_kernel, grid, block, 0, stream, a, b, 0u, (const float4 *)in, (float4 *)out,
+                              nr, nw);
+    else
+        hipLaunchKernelGGL(probe_copy_kernel, grid, block, 0, stream, (const float4 *)in, (float4 *)out, nr, nw);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
 // launch wrappers (called from sng_api.cpp)
 // ---------------------------------------------------------------------------------
 // Optional start/stop events: hipExtLaunchKernel stamps them with the dispatch's own
@@ -1539,6 +1752,35 @@ static void launch_lean(const Params &p, const DeviceState &s, const InfoPtrs &i
                          : (req ? step_lean_kernel<NC, false, true> : step_lean_kernel<NC, false, false>);
     const dim3 grid((unsigned)((E + kLeanBlock - 1) / kLeanBlock)), block(kLeanBlock);
     const uint32_t lds = (uint32_t)LeanLds<NC>::BYTES;
+    if (ev)
+        hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,
+                              vec_io, k, p, s, info);
+    else
+        hipLaunchKernelGGL(kern, grid, block, lds, stream, act, obs, reward, done, E, t, vec_io, k, p, s, info);
+}
+
+// The wide lean step kernel's configurations: N = 50 (BASELINE config 5's station), one lane per env, no
+// diagnostics, NumPy-2 promotion with a power-of-two dt; stochastic profiles allowed.
+static bool wide_step(const Params &p, bool diag) {
+    return p.n == 50 && !diag && !p.legacy && p.dt_pow2 && !(p.lanes == 2 || p.lanes == 4);
+}
+
+template <int NC>
+static void launch_wide(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
+                        const float *act, float *obs, double *reward, uint8_t *done, int64_t E, int t, int vec_io,
+                        hipStream_t stream, const LaunchEvents *ev) {
+    StepConst k;
+    for (int i = 0; i < CST_COUNT; ++i) k.v[i] = step_constant(&tab, t, i);
+    const bool req = p.req_stream && !p.req_zero;
+    const int v = (p.packed ? 4 : 0) | (req ? 2 : 0) | (p.noise ? 1 : 0);
+    void (*kerns[8])(const float *, float *, double *, uint8_t *, int64_t, int, int, StepConst, Params, DeviceState,
+                     InfoPtrs) = {step_wide_kernel<NC, false, false, false>, step_wide_kernel<NC, false, false, true>,
+                                  step_wide_kernel<NC, false, true, false>,  step_wide_kernel<NC, false, true, true>,
+                                  step_wide_kernel<NC, true, false, false>,  step_wide_kernel<NC, true, false, true>,
+                                  step_wide_kernel<NC, true, true, false>,   step_wide_kernel<NC, true, true, true>};
+    auto kern = kerns[v];
+    const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
+    const uint32_t lds = (uint32_t)WideLds<NC>::BYTES;
     if (ev)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,
                               vec_io, k, p, s, info);
@@ -1632,6 +1874,10 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
         launch_lean_n(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
         return hipGetLastError();
     }
+    if (wide_step(p, info_diag(info))) {
+        launch_wide<50>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
+        return hipGetLastError();
+    }
 #endif
     if (info_diag(info))
         launch_step_n<true>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev);
@@ -1647,6 +1893,9 @@ int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) 
     if (lean_step(p, info_diag(info)))
         return snprintf(buf, (size_t)len, "void sng::step_lean_kernel<%d, %s, %s>", p.n, p.packed ? "true" : "false",
                         (p.req_stream && !p.req_zero) ? "true" : "false");
+    if (wide_step(p, info_diag(info)))
+        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %s, %s, %s>", p.n, p.packed ? "true" : "false",
+                        (p.req_stream && !p.req_zero) ? "true" : "false", p.noise ? "true" : "false");
 #endif
     int nc = 0, lanes = 1;
     switch (p.n) {

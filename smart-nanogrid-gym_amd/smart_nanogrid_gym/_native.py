@@ -140,6 +140,8 @@ EXPORTS = {
                                                    c_int32_p, c_int32_p, ctypes.c_int32, c_double_p]),
     "sng_host_threads": (ctypes.c_int32, []),
     "sng_get_day_counter": (ctypes.c_int, [_H, ctypes.POINTER(ctypes.c_uint64), _S]),
+    "sng_bandwidth_probe": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
+                                           ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), _S]),
     "sng_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "sng_comm_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                        ctypes.POINTER(ctypes.c_void_p)]),

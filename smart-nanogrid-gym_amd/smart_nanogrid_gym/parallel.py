@@ -58,15 +58,23 @@ class DayReturnExchange:
     issued asynchronously so it runs on the collective stream while the next replay's kernels
     run.  Two snapshot buffers alternate (one EpisodeGraph per buffer, via its day_returns):
     before buffer k is refilled, acquire(k) makes the compute stream wait for the gather that
-    reads it (work.wait() orders streams; the host does not block on NCCL/RCCL)."""
+    reads it (work.wait() orders streams; the host does not block on NCCL/RCCL).
 
-    def __init__(self, days, envs, device, group=None):
+    staging="host" (gloo, which gathers host tensors; several ranks sharing one GPU): gather(k) copies
+    the snapshot into pinned host memory once the replay that fills it is done and gathers that copy, so
+    acquire(k) has nothing left to wait for on the device."""
+
+    def __init__(self, days, envs, device, group=None, staging="device"):
         self.group = group
         self.world = dist.get_world_size(group)
-        check_equal_shards(envs, device=device, group=group)
-        self.fused = _fused_gather(group)
+        self.host = staging == "host"
+        check_equal_shards(envs, device=None if self.host else device, group=group)
+        self.fused = _fused_gather(group) and not self.host
         self.snap = [torch.zeros((days, envs), dtype=torch.float64, device=device) for _ in range(2)]
-        self.out = [torch.empty((self.world, days, envs), dtype=torch.float64, device=device) for _ in range(2)]
+        odev = "cpu" if self.host else device
+        self.out = [torch.empty((self.world, days, envs), dtype=torch.float64, device=odev) for _ in range(2)]
+        self.staged = ([torch.empty((days, envs), dtype=torch.float64, pin_memory=True) for _ in range(2)]
+                       if self.host else None)
         self.work = [None, None]
         self.gathers = 0
 
@@ -79,7 +87,12 @@ class DayReturnExchange:
 
     def gather(self, k):
         """Start the all-gather of buffer k (after the replay that fills it has been launched)."""
-        if self.fused:
+        if self.host:
+            self.staged[k].copy_(self.snap[k], non_blocking=True)
+            torch.cuda.current_stream(self.snap[k].device).synchronize()
+            self.work[k] = dist.all_gather(list(self.out[k].unbind(0)), self.staged[k], group=self.group,
+                                           async_op=True)
+        elif self.fused:
             self.work[k] = dist.all_gather_into_tensor(self.out[k], self.snap[k], group=self.group, async_op=True)
         else:
             self.work[k] = dist.all_gather(list(self.out[k].unbind(0)), self.snap[k], group=self.group,

@@ -108,3 +108,25 @@ def test_native_rccl_exchange_world1():
         venv.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_bench_world2_branch_on_one_gpu():
+    """bench.py's own world > 1 branch (process group, two alternating day graphs writing
+    per-day return rows, the overlapped DayReturnExchange, max-over-ranks timing and the gathered-returns
+    asserts) run by torch.distributed.run with two ranks sharing this box's one GPU.  RCCL needs a GPU per
+    rank, so the ranks gather over gloo with the snapshots staged through host memory
+    (--dist-backend gloo); the 8-GPU driver run takes the RCCL path of the same code."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--steps", "4", "--warmup", "2", "--envs", "4096", "--dist-backend", "gloo",
+           "--no-cpu-baseline", "--timing-days", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 4 and out["value"] > 0
+    assert out["config"]["envs_per_gpu"] == 4096 and "env-sharded x2" in out["config"]["parallelism"]

@@ -57,17 +57,25 @@ def _seq(x):
     return s
 
 
-@pytest.mark.parametrize("N,v2x", [(10, True), (16, True), (8, True), (10, False)])
+@pytest.mark.parametrize("N,v2x", [(10, True), (16, True), (8, True), (10, False), (50, True), (50, False)])
 def test_lean_totals_vs_general_kernel_and_oracle(N, v2x):
+    """N = 50 is BASELINE config 5's station (15-minute steps, extended day, stochastic profiles), stepped by
+    the wide lean kernel: running sums where exact, the positive powers rebuilt from the records and the
+    actions where not, and a wavefront with a discharging action in numpy's order throughout."""
     E, seed = 2048, 4242 + N
     kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
               vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
               battery_system_available_in_model=True, vehicle_to_everything=v2x)
+    if N == 50:
+        kw.update(time_interval="15min", extended_day=True, pv_noise=0.2, price_noise=0.1)
     lean = SmartNanogridVecEnv(E, seed=seed, rng="reference", **kw)
     lean._info.flags = None
     diag = SmartNanogridVecEnv(E, seed=seed, rng="reference", info=True, **kw)
     diag._enable_info(per_charger=True)
-    assert lean.step_kernel_name() == f"void sng::step_lean_kernel<{N}, false, false>"
+    want = (f"void sng::step_wide_kernel<{N}, false, false, true>" if N == 50
+            else f"void sng::step_lean_kernel<{N}, false, false>")
+    assert lean.step_kernel_name() == want
+    T = lean.timesteps
     ids = np.arange(0, E, 16)
     cfg = O.OracleConfig(**kw)
     envs = [O.OracleEnv(cfg, seed + int(i)) for i in ids]
@@ -78,7 +86,7 @@ def test_lean_totals_vs_general_kernel_and_oracle(N, v2x):
         o_d = diag.reset_tensors().cpu().numpy()
         np.testing.assert_array_equal(o_l, o_d)
         np.testing.assert_array_equal(o_l[ids], np.stack([e.reset() for e in envs]))
-        for t in range(24):
+        for t in range(T):
             a = _actions(rng, E, N, v2x)
             ad = torch.from_numpy(a).to(lean.device)
             ol, rl, _ = lean.step_tensors(ad)
