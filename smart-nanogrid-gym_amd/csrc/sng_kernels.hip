@@ -21,6 +21,8 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <type_traits>
+
 #include "sng.h"
 #include "sng_layout.h"
 
@@ -791,11 +793,17 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
 //   - constants by value, one kernarg round trip before the loads, 1/cap by recip_cap, no LDS but the
 //     actions and observation tiles (40 KB per wavefront: four per CU).
 // ---------------------------------------------------------------------------------
-template <int NC>
+#ifndef SNG_WIDE_SB
+#define SNG_WIDE_SB 1
+#endif
+constexpr int kWideSB = SNG_WIDE_SB;   // chargers per scheduling group of the wide kernel's fast loop
+
+template <int NC, int L>
 struct WideLds {
-    static constexpr int A = NC + 1;   // actions per env with a BESS (one fewer without)
+    static constexpr int WENVS = kWave / L;   // envs per wavefront
+    static constexpr int A = NC + 1;          // actions per env with a BESS (one fewer without)
     static constexpr int O = 2 * NC + 9;
-    static constexpr int ACT = round4(kWave * A), OBS = round4(kWave * O);
+    static constexpr int ACT = round4(WENVS * A), OBS = round4(WENVS * O);
     static constexpr size_t BYTES = (size_t)(ACT + OBS) * 4;
 };
 
@@ -804,24 +812,61 @@ __device__ __forceinline__ double charging_power(const Params &p, float a) {
     return (double)__fmul_rn(__fmul_rn(a, p.ev_power_f), p.ev_eff_f);
 }
 
-template <int NC, bool PK, bool REQ, bool NOISE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) void step_wide_kernel(
+// Lane `part` K's value of an env's L adjacent lanes (L = 2 or 4), for the env's first lane, by DPP quad
+// permutation (the env's lanes never straddle a quad).
+template <int L, int K>
+__device__ __forceinline__ uint32_t from_part(uint32_t x) {
+    constexpr int ctrl = L == 2 ? (K | (K << 2) | ((K + 2) << 4) | ((K + 2) << 6)) : (K | (K << 2) | (K << 4) | (K << 6));
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, ctrl, 0xF, 0xF, false);
+}
+template <int L, int K>
+__device__ __forceinline__ double from_part(double x) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, x);
+    const uint64_t lo = from_part<L, K>((uint32_t)b), hi = from_part<L, K>((uint32_t)(b >> 32));
+    return __builtin_bit_cast(double, lo | (hi << 32));
+}
+
+// L lanes per env (1, 2 or 4): lane `part` of an env steps chargers [part * CPL, min(NC, (part + 1) * CPL)),
+// CPL = ceil(NC / L).  The env's lanes are adjacent (one DPP quad); the partial charging sums, counts and
+// minima combine exactly on the first lane (a sum the exactness test accepts is exact in any order, and
+// fewer than 8 powers are numpy's in-order sum when one lane holds them all), the first lane adds the
+// other lanes' vehicle penalties after its own in charger order (Python's sum, penaliser.py:55), and the
+// rare exact-order paths run on the first lane over all chargers.
+template <int NC, int L, bool PK, bool REQ, bool NOISE>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(L, L))) void step_wide_kernel(
     const float *__restrict__ act, float *__restrict__ obs, double *__restrict__ reward, uint8_t *__restrict__ done,
     int64_t E, int t, int vec_io, StepConst k, Params p, DeviceState s, InfoPtrs info) {
-    using Lay = WideLds<NC>;
-    constexpr int KT = (Lay::A * kWave + 4 * kWave - 1) / (4 * kWave);
+    static_assert(L == 1 || L == 2 || L == 4, "one, two or four lanes per env");
+    using Lay = WideLds<NC, L>;
+    constexpr int WENVS = Lay::WENVS, CPL = (NC + L - 1) / L;
+    static_assert((L - 1) * CPL < NC, "every lane steps at least one charger");
+    constexpr int KT = (Lay::A * WENVS + 4 * kWave - 1) / (4 * kWave);
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int Ad = p.act_dim, O = p.obs_dim;
-    const int lane = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * kWave;   // the grid covers E exactly: every wave has an env
-    const int nw = (E - e0) < kWave ? (int)(E - e0) : kWave;
-    const bool live = lane < nw;
+    const int lane = threadIdx.x, le = lane / L, part = lane % L;
+    const bool leader = part == 0;
+    const int64_t e0 = (int64_t)blockIdx.x * WENVS;   // the grid covers E exactly: every wave has an env
+    const int nw = (E - e0) < WENVS ? (int)(E - e0) : WENVS;
+    const bool live = le < nw;
     float *s_act = lds;
     float *s_obs = lds + Lay::ACT;
-    const int64_t el = live ? e0 + lane : E - 1;   // idle lanes load a valid env and discard it
+    const int64_t el = live ? e0 + le : E - 1;   // idle lanes load a valid env and discard it
     const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;
     const size_t plane = (size_t)t * NC * (size_t)E;   // this step's timeline planes
     const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
+    const int c0 = part * CPL;
+    const int nc = (NC - c0) < CPL ? NC - c0 : CPL;   // the lane's chargers (the last lane's range is ragged)
+    // the lane's first charger row as a per-lane byte offset; charger j of the lane adds j * E (uniform).
+    // Past the lane's range (j >= nc) the loads re-read its first charger and nothing is stored.
+    const uint32_t row4 = el4 + (uint32_t)c0 * (uint32_t)E * 4u;
+    const uint32_t row4_last = el4 + (uint32_t)(NC - 1) * (uint32_t)E * 4u;
+    // the (per-lane, uniform) byte offsets of charger j of the lane: j * E in the uniform part, except for
+    // the j some lane lacks (a ragged last lane), where the per-lane part carries it
+    auto ragged = [](int j) { return NC % L != 0 && j >= NC - (L - 1) * CPL; };
+    auto r4_of = [&](int j) -> uint32_t { return ragged(j) ? 0u : (uint32_t)j * (uint32_t)E * 4u; };
+    auto row_of = [&](int j) -> uint32_t {
+        return ragged(j) ? (j < nc ? row4 + (uint32_t)j * (uint32_t)E * 4u : row4_last) : row4;
+    };
 
     // loads oldest-needed-first: the actions tile and the per-env values, then every charger's state
     TileStage<KT, kWave> act_tile;
@@ -839,35 +884,36 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
             fpr[j] = bld(s.prof + pp + (size_t)(t + j) * E, el8);
         }
     }
-    uint32_t w[NC];
-    double aux[PK ? 1 : NC], run[NC], req[NC];
+    uint32_t w[CPL];
+    double aux[PK ? 1 : CPL], run[CPL], req[CPL];
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
+    for (int j = 0; j < CPL; ++j) {
+        // charger c0 + j (past a ragged lane's range: its charger NC - 1 again, discarded)
+        const uint32_t v4 = row_of(j), r4 = r4_of(j), v8 = 2u * v4, r8 = 2u * r4;
         if (PK) {
-            w[c] = bld(rec_t, el4, r4);
+            w[j] = bld(rec_t, v4, r4);
         } else {
-            w[c] = bld(s.word + plane, el4, r4);
-            aux[PK ? 0 : c] = bld(s.aux + plane, el8, r8);
+            w[j] = bld(s.word + plane, v4, r4);
+            aux[PK ? 0 : j] = bld(s.aux + plane, v8, r8);
         }
-        run[c] = bld(s.soc, el8, r8);
-        req[c] = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
+        run[j] = bld(s.soc, v8, r8);
+        req[j] = REQ ? bld(s.req + plane, v8, r8) : (p.req_zero ? 0.0 : 1.0);
     }
     act_tile.commit(s_act, lane);
     wave_lds_fence();
 
-    const float *a_row = s_act + lane * Ad;
-    float *o_row = s_obs + lane * O;
-    float av[NC];
+    const float *a_row = s_act + le * Ad;
+    float *o_row = s_obs + le * O;
+    float av[CPL];
     float amin = 0.0f;
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        av[c] = a_row[c];
-        amin = __builtin_fminf(amin, av[c]);   // a NaN action is not negative (fmin drops it)
+    for (int j = 0; j < CPL; ++j) {
+        av[j] = a_row[(c0 + j) < NC ? c0 + j : NC - 1];
+        amin = __builtin_fminf(amin, av[j]);   // a NaN action is not negative (fmin drops it)
     }
     const float bess_action = p.bess ? a_row[NC] : 0.0f;
     const int k_soc = p.pv ? 8 : 4;
-    if (live) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, fpv, fpr);
+    if (live && leader) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, fpv, fpr);
 
     double pen_v = 0.0, p_ch = 0.0, p_dis = 0.0;
     uint32_t n_nonexist = 0, fl = 0;
@@ -875,29 +921,69 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
         // the fast loop: no negative action in the wave, so no negative power (p_dis stays 0.0)
         double seq_pos = 0.0, pmin = __builtin_inf();
         int n_pos = 0;
+        double qv[L > 1 ? CPL : 1];
         if (live) {
 #pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const uint32_t capi = (w[c] >> W_CAP_SHIFT) & 0xffu;
-                const bool occ = (w[c] & W_OCC) != 0;
-                const ChargerResult r = charger_step<true, true>(p, PK ? (w[c] & ~W_STATIC) : w[c],
-                                                                 PK ? 0.0 : aux[PK ? 0 : c], run[c], req[c], av[c], t,
+            for (int j = 0; j < CPL; ++j) {
+                const int c = c0 + j;
+                if (NC % L != 0 && j >= nc) {   // a ragged lane's range ends: adds nothing
+                    qv[L > 1 ? j : 0] = 0.0;
+                    continue;
+                }
+                const uint32_t capi = (w[j] >> W_CAP_SHIFT) & 0xffu;
+                const bool occ = (w[j] & W_OCC) != 0;
+                const ChargerResult r = charger_step<true, true>(p, PK ? (w[j] & ~W_STATIC) : w[j],
+                                                                 PK ? 0.0 : aux[PK ? 0 : j], run[j], req[j], av[j], t,
                                                                  recip_cap((double)capi));
-                bst<kNT>(s.soc, el8, (PK && !occ) ? (double)rec_soc(w[c]) : r.soc, (uint32_t)c * (uint32_t)E * 8u);
+                bst<kNT>(s.soc, 2u * row_of(j), (PK && !occ) ? (double)rec_soc(w[j]) : r.soc, 2u * r4_of(j));
                 o_row[k_soc + c] = (float)r.soc;
-                o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[c]);
+                o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[j]);
                 n_nonexist += r.nx;
                 fl |= r.fl;
+                if (L > 1) qv[L > 1 ? j : 0] = r.q;
                 pen_v += r.q;
                 const bool ip = r.pw > 0.0;
                 seq_pos += __builtin_fmax(r.pw, 0.0);
                 n_pos += ip ? 1 : 0;
                 pmin = __builtin_fmin(pmin, ip ? r.pw : __builtin_inf());
-                __builtin_amdgcn_sched_barrier(0);   // charger c waits only for its own loads
+                // chargers in order (groups of kWideSB): charger j waits only for its own loads
+                if ((j + 1) % kWideSB == 0) __builtin_amdgcn_sched_barrier(0);
             }
         }
+        // numpy sums fewer than 8 positive powers in order: one lane's running sum is that sum; two lanes'
+        // partial sums combined are that sum only when one of them is empty or the sum is exact
+        bool split = false;
+        if constexpr (L > 1) {
+            // the other lanes' totals (exact combinations), and their penalties after the first lane's own,
+            // in charger order (adding a +0.0 term is exact)
+            const double seq_own = seq_pos, pmin_own = pmin;
+            const int n_own = n_pos;
+            const uint32_t nx_own = n_nonexist, fl_own = fl;
+            int with_pos = n_own > 0 ? 1 : 0;
+            auto gather = [&](auto kc) {
+                constexpr int K = decltype(kc)::value;
+                const int nk = (int)from_part<L, K>((uint32_t)n_own);
+                with_pos += nk > 0 ? 1 : 0;
+                n_pos += nk;
+                seq_pos += from_part<L, K>(seq_own);
+                pmin = __builtin_fmin(pmin, from_part<L, K>(pmin_own));
+                n_nonexist += from_part<L, K>(nx_own);
+                fl |= from_part<L, K>(fl_own);
+#pragma unroll
+                for (int j = 0; j < CPL; ++j) {
+                    const double qk = from_part<L, K>(qv[L > 1 ? j : 0]);
+                    pen_v = leader ? pen_v + qk : pen_v;
+                }
+            };
+            gather(std::integral_constant<int, 1>{});
+            if constexpr (L > 2) {
+                gather(std::integral_constant<int, 2>{});
+                gather(std::integral_constant<int, 3>{});
+            }
+            split = with_pos > 1;
+        }
         p_ch = seq_pos;
-        const bool pos_slow = live && n_pos >= 8 && !(seq_pos <= pmin * 0x1.0p28);
+        const bool pos_slow = live && leader && (n_pos >= 8 || split) && !(seq_pos <= pmin * 0x1.0p28);
         if (__builtin_amdgcn_ballot_w64(pos_slow)) {   // wave-uniform: rare
             if (pos_slow) {
                 // the compacted positive powers again, in charger order: an occupied charger charging with
@@ -917,11 +1003,11 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
         }
     } else {
         // a wave with a discharging action: numpy's pairwise order for both signs (PairwiseSum), one
-        // charger at a time, its inputs re-read from memory and the actions tile
+        // charger at a time on the env's first lane, its inputs re-read from memory and the actions tile
         PairwiseSum pos, neg;
         pos.init();
         neg.init();
-        if (live) {
+        if (live && leader) {
 #pragma unroll 1
             for (int c = 0; c < NC; ++c) {
                 const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
@@ -946,9 +1032,9 @@ __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) v
         p_ch = pos.result();
         p_dis = neg.result();
     }
-    if (live) {
+    if (live && leader) {
         pen_v += (t == 0) ? pen0_l : 0.0;   // python index -1 slot; every per-charger term is 0 at t = 0
-        env_tail<false>(p, s, info, e0, (uint32_t)lane, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action, p_ch,
+        env_tail<false>(p, s, info, e0, (uint32_t)le, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action, p_ch,
                         p_dis, pen_v, 100.0 * (double)n_nonexist, fl, o_row, k.v, fpv, fpr,
                         info.episode_return ? ret_l : 0.0, 0.0, reward, done);
     }
@@ -1765,22 +1851,33 @@ static bool wide_step(const Params &p, bool diag) {
     return p.n == 50 && !diag && !p.legacy && p.dt_pow2 && !(p.lanes == 2 || p.lanes == 4);
 }
 
+// Lanes per env of the wide lean step kernel: two (2,048 wavefronts at 65,536 envs, two per SIMD).
+// A/B at config 5 (tools/wide_ab.sh, two runs each): 1 lane 25.85-25.91 us per step in the day graph,
+// 2 lanes 22.54-22.62, 4 lanes 30.36-30.49 (128 VGPRs: 40 spilled to scratch).
+#ifndef SNG_WIDE_L
+#define SNG_WIDE_L 2
+#endif
+constexpr int kWideL = SNG_WIDE_L;
+
 template <int NC>
 static void launch_wide(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
                         const float *act, float *obs, double *reward, uint8_t *done, int64_t E, int t, int vec_io,
                         hipStream_t stream, const LaunchEvents *ev) {
+    constexpr int L = kWideL;
     StepConst k;
     for (int i = 0; i < CST_COUNT; ++i) k.v[i] = step_constant(&tab, t, i);
     const bool req = p.req_stream && !p.req_zero;
     const int v = (p.packed ? 4 : 0) | (req ? 2 : 0) | (p.noise ? 1 : 0);
     void (*kerns[8])(const float *, float *, double *, uint8_t *, int64_t, int, int, StepConst, Params, DeviceState,
-                     InfoPtrs) = {step_wide_kernel<NC, false, false, false>, step_wide_kernel<NC, false, false, true>,
-                                  step_wide_kernel<NC, false, true, false>,  step_wide_kernel<NC, false, true, true>,
-                                  step_wide_kernel<NC, true, false, false>,  step_wide_kernel<NC, true, false, true>,
-                                  step_wide_kernel<NC, true, true, false>,   step_wide_kernel<NC, true, true, true>};
+                     InfoPtrs) = {
+        step_wide_kernel<NC, L, false, false, false>, step_wide_kernel<NC, L, false, false, true>,
+        step_wide_kernel<NC, L, false, true, false>,  step_wide_kernel<NC, L, false, true, true>,
+        step_wide_kernel<NC, L, true, false, false>,  step_wide_kernel<NC, L, true, false, true>,
+        step_wide_kernel<NC, L, true, true, false>,   step_wide_kernel<NC, L, true, true, true>};
     auto kern = kerns[v];
-    const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
-    const uint32_t lds = (uint32_t)WideLds<NC>::BYTES;
+    constexpr int WENVS = WideLds<NC, L>::WENVS;
+    const dim3 grid((unsigned)((E + WENVS - 1) / WENVS)), block(kWave);
+    const uint32_t lds = (uint32_t)WideLds<NC, L>::BYTES;
     if (ev)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,
                               vec_io, k, p, s, info);
@@ -1894,8 +1991,9 @@ int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) 
         return snprintf(buf, (size_t)len, "void sng::step_lean_kernel<%d, %s, %s>", p.n, p.packed ? "true" : "false",
                         (p.req_stream && !p.req_zero) ? "true" : "false");
     if (wide_step(p, info_diag(info)))
-        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %s, %s, %s>", p.n, p.packed ? "true" : "false",
-                        (p.req_stream && !p.req_zero) ? "true" : "false", p.noise ? "true" : "false");
+        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %d, %s, %s, %s>", p.n, kWideL,
+                        p.packed ? "true" : "false", (p.req_stream && !p.req_zero) ? "true" : "false",
+                        p.noise ? "true" : "false");
 #endif
     int nc = 0, lanes = 1;
     switch (p.n) {

@@ -72,9 +72,11 @@ def test_lean_totals_vs_general_kernel_and_oracle(N, v2x):
     lean._info.flags = None
     diag = SmartNanogridVecEnv(E, seed=seed, rng="reference", info=True, **kw)
     diag._enable_info(per_charger=True)
-    want = (f"void sng::step_wide_kernel<{N}, false, false, true>" if N == 50
-            else f"void sng::step_lean_kernel<{N}, false, false>")
-    assert lean.step_kernel_name() == want
+    name = lean.step_kernel_name()
+    if N == 50:
+        assert name.startswith("void sng::step_wide_kernel<50, ") and name.endswith(", false, false, true>"), name
+    else:
+        assert name == f"void sng::step_lean_kernel<{N}, false, false>"
     T = lean.timesteps
     ids = np.arange(0, E, 16)
     cfg = O.OracleConfig(**kw)
