@@ -1820,10 +1820,22 @@ struct LaunchEvents {
     hipEvent_t start = nullptr, stop = nullptr;
 };
 
+// Stations of 10 chargers without V2X (the headline configuration) step through the wide kernel with two
+// lanes per env: A/B at 65,536 x 10 x 24 (tools/ab_headline.sh, three runs each) 6.47-6.51 us per step
+// in the day graph vs 6.67-6.71 for the lean kernel, day 0.1749-0.1761 vs 0.1796-0.1803 ms; one lane per
+// env 6.75-6.79, four 8.15-8.23.  With V2X a discharging action is routine, and the lean kernel's LDS rows
+// keep numpy's order cheaper than the wide kernel's rolled re-read.  SNG_WIDE_N10=0 builds the lean path.
+#ifndef SNG_WIDE_N10
+#define SNG_WIDE_N10 1
+#endif
+#ifndef SNG_WIDE_L10
+#define SNG_WIDE_L10 2
+#endif
 // The lean step kernel's configurations: a compile-time station of N <= 16, one lane per env, no
 // diagnostics, NumPy-2 promotion with a power-of-two dt, no stochastic profiles.
 static bool lean_step(const Params &p, bool diag) {
-    const bool nc = p.n == 1 || p.n == 2 || p.n == 4 || p.n == 8 || p.n == 10 || p.n == 16;
+    const bool nc = p.n == 1 || p.n == 2 || p.n == 4 || p.n == 8 || (p.n == 10 && (!SNG_WIDE_N10 || p.v2x)) ||
+                    p.n == 16;
     return nc && !diag && !p.legacy && p.dt_pow2 && !p.noise && !(p.lanes == 2 || p.lanes == 4);
 }
 
@@ -1848,7 +1860,8 @@ static void launch_lean(const Params &p, const DeviceState &s, const InfoPtrs &i
 // The wide lean step kernel's configurations: N = 50 (BASELINE config 5's station), one lane per env, no
 // diagnostics, NumPy-2 promotion with a power-of-two dt; stochastic profiles allowed.
 static bool wide_step(const Params &p, bool diag) {
-    return p.n == 50 && !diag && !p.legacy && p.dt_pow2 && !(p.lanes == 2 || p.lanes == 4);
+    return (p.n == 50 || (SNG_WIDE_N10 && p.n == 10 && !p.noise && !p.v2x)) && !diag && !p.legacy && p.dt_pow2 &&
+           !(p.lanes == 2 || p.lanes == 4);
 }
 
 // Lanes per env of the wide lean step kernel: two (2,048 wavefronts at 65,536 envs, two per SIMD).
@@ -1858,12 +1871,13 @@ static bool wide_step(const Params &p, bool diag) {
 #define SNG_WIDE_L 2
 #endif
 constexpr int kWideL = SNG_WIDE_L;
+__host__ __device__ constexpr int wide_lanes(int NC) { return NC == 10 ? SNG_WIDE_L10 : kWideL; }
 
 template <int NC>
 static void launch_wide(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
                         const float *act, float *obs, double *reward, uint8_t *done, int64_t E, int t, int vec_io,
                         hipStream_t stream, const LaunchEvents *ev) {
-    constexpr int L = kWideL;
+    constexpr int L = wide_lanes(NC);
     StepConst k;
     for (int i = 0; i < CST_COUNT; ++i) k.v[i] = step_constant(&tab, t, i);
     const bool req = p.req_stream && !p.req_zero;
@@ -1972,7 +1986,10 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
         return hipGetLastError();
     }
     if (wide_step(p, info_diag(info))) {
-        launch_wide<50>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
+        if (p.n == 10)
+            launch_wide<10>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
+        else
+            launch_wide<50>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
         return hipGetLastError();
     }
 #endif
@@ -1991,7 +2008,7 @@ int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) 
         return snprintf(buf, (size_t)len, "void sng::step_lean_kernel<%d, %s, %s>", p.n, p.packed ? "true" : "false",
                         (p.req_stream && !p.req_zero) ? "true" : "false");
     if (wide_step(p, info_diag(info)))
-        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %d, %s, %s, %s>", p.n, kWideL,
+        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %d, %s, %s, %s>", p.n, wide_lanes(p.n),
                         p.packed ? "true" : "false", (p.req_stream && !p.req_zero) ? "true" : "false",
                         p.noise ? "true" : "false");
 #endif

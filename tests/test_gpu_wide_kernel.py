@@ -53,8 +53,8 @@ def test_wide_step_kernel_device_days_vs_oracle_and_general(E, sample):
         name = venv.step_kernel_name()
         assert name.startswith(WIDE_KERNEL[0]) and name.endswith(WIDE_KERNEL[1]), name
         np.testing.assert_array_equal(obs, diag.reset_tensors().cpu().numpy())
-        ivs, ratios = venv.get_scenarios(0, E)
-        ref0 = np.stack([load_day(e, ivs[i], ratios[i]) for e, i in zip(envs, ids)])
+        days = [venv.get_scenario(int(i)) for i in ids]   # the sampled envs' days only
+        ref0 = np.stack([load_day(e, iv, ratio) for e, (iv, ratio) in zip(envs, days)])
         np.testing.assert_array_equal(obs[ids], ref0, err_msg=f"day {day} reset")
         for t in range(venv.timesteps):
             a = actions(rng, E, 51, heavy)

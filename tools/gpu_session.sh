@@ -36,6 +36,8 @@ for s in $STEPS; do
     cfg5)  run bench_cfg5 600 python bench.py --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 --cpu-budget 12
            run prof_cfg5 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_cfg5 -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 ;;
     closed) run closed_loop 600 python tools/closed_loop_bench.py ;;
+    memfloor) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_memfloor.so run memfloor 300 python bench.py --no-cpu-baseline
+           SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_memfloor.so run memfloor_cfg5 300 python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 ;;
     reset) run reset_bench 600 python tools/reset_bench.py ;;
     pmc5)  run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc5_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 2 --warmup 1 --graph-days 1 --timing-days 1
            run pmc5_write 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc5_write -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 2 --warmup 1 --graph-days 1 --timing-days 1 ;;
