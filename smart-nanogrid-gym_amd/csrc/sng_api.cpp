@@ -40,8 +40,10 @@ hipError_t launch_bump_day(const DeviceState &s, hipStream_t stream);
 hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, hipStream_t stream, hipEvent_t a,
                              hipEvent_t b);
 hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream);
+hipError_t launch_mt_prepare(const RefStreams &rs, int64_t E, hipStream_t stream);
+hipError_t launch_py_ratio(const RefStreams &ps, double *ratio, int64_t E, int end_draw, int draw, hipStream_t stream);
 hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
-                          int i1, hipStream_t stream);
+                          int i1, bool prepare, hipStream_t stream);
 int step_lanes_supported(int n, int lanes);
 int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len);
 }  // namespace sng
@@ -504,7 +506,15 @@ struct SngEnv {
     // drawn by ref_day_kernel), Python's on the host (two or three draws a day)
     RefStreams rs{};
     bool np_seeded = false;
-    std::vector<MT19937> py_rng;
+    // the next day's stream blocks are prepared (mt_prepare_kernel) on a side stream while a day is stepped;
+    // every access to rs on a caller's stream first waits for prep_done
+    hipStream_t prep_stream = nullptr;
+    hipEvent_t prep_done = nullptr, day_drawn = nullptr;
+    bool prep_launched = false;   // prep_done marks a prepare launched on prep_stream
+
+    bool prepared = false;        // the next day's blocks are (being) prepared: no inline prepare
+    RefStreams ps{};                  // Python's `random` stream of every env, on the device (py_ratio_kernel)
+    bool py_seeded = false;
     std::string err;
 
     size_t timeline() const { return (size_t)p.T * p.n * (size_t)E; }
@@ -600,31 +610,47 @@ int ensure_staging(SngEnv *env, bool with_req) {
 }
 
 // The reference's global RNG streams of every env, np.random.seed(s) and random.seed(s) with
-// s = seed + global env index (SngRngMode SNG_RNG_REFERENCE): Python's on the host ...
-void ensure_streams(SngEnv *env) {
-    if (!env->py_rng.empty()) return;
-    env->py_rng.resize(env->E);
+// s = seed + global env index (SngRngMode SNG_RNG_REFERENCE), both on the device.  Python's is seeded on
+// the host threads (CPython's init_by_array, sng_mt.h) and uploaded once into the RefStreams layout
+// (block 0, position N: the first draw twists), then drawn by py_ratio_kernel: random.randint(0, 180)
+// for a reset's PV ratio, after the day-end draw the last step owes (smart_nanogrid_environment.py:181, 349).
+int await_prepare(SngEnv *env, hipStream_t st);
+int ensure_py_streams(SngEnv *env, hipStream_t st) {
+    const size_t E = (size_t)env->E;
+    if (!env->ps.mt) {
+        HIP_TRY(env, hipMalloc(&env->ps.mt, E * 2 * kMtN * sizeof(uint32_t)));
+        HIP_TRY(env, hipMalloc(&env->ps.pos, E * sizeof(int32_t)));
+    }
+    if (env->py_seeded) return SNG_OK;
+    int rc = await_prepare(env, st);   // no preparation may still be writing the streams
+    if (rc) return rc;
+    std::vector<uint32_t> words(E * kMtN);
+    std::vector<int32_t> pos(E);
     const uint64_t s0 = env->seed + (uint64_t)env->p.env_offset;
-    parallel_ranges(env->E, 1024, [env, s0](int64_t b, int64_t en) {
-        for (int64_t i = b; i < en; ++i) env->py_rng[i].seed_python(s0 + (uint64_t)i);
-    });
-}
-
-// random_pv_shift_ratio = random.randint(0, 180) / 100 from every env's Python stream
-// (smart_nanogrid_environment.py:349), after the day-end draw the last step still owes (:181),
-// into the pinned h_ratio; the streams are independent, so host threads take ranges of envs.
-void draw_ratios(SngEnv *env) {
-    const bool end_draw = env->day_finished;
-    parallel_ranges(env->E, 4096, [env, end_draw](int64_t b, int64_t en) {
-        // the streams are 2.5 KB apart: two prefetch stages (the position word 16 streams ahead, the
-        // next state word 8 ahead) keep the misses of many streams in flight
+    parallel_ranges(env->E, 1024, [&](int64_t b, int64_t en) {
+        MT19937 m;
+        uint32_t st_words[MT19937::kStateWords];
         for (int64_t i = b; i < en; ++i) {
-            if (i + 16 < en) __builtin_prefetch(env->py_rng[i + 16].pos_addr());
-            if (i + 8 < en) __builtin_prefetch(env->py_rng[i + 8].next_addr());
-            if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
-            env->h_ratio[i] = (double)env->py_rng[i].py_randint(0, 180) / 100;
+            m.seed_python(s0 + (uint64_t)i);
+            m.save(st_words);
+            std::memcpy(words.data() + (size_t)i * kMtN, st_words, kMtN * sizeof(uint32_t));
+            pos[i] = (int32_t)st_words[kMtN];   // block 0, mti = N
         }
     });
+    HIP_TRY(env, hipMemcpy2DAsync(env->ps.mt, 2 * kMtN * sizeof(uint32_t), words.data(), kMtN * sizeof(uint32_t),
+                                  kMtN * sizeof(uint32_t), E, hipMemcpyHostToDevice, st));
+    HIP_TRY(env, hipMemcpyAsync(env->ps.pos, pos.data(), E * sizeof(int32_t), hipMemcpyHostToDevice, st));
+    // the first twist by a wavefront per env now, not by py_ratio_kernel's one lane at the first draw
+    HIP_TRY(env, launch_mt_prepare(env->ps, env->E, st));
+    HIP_TRY(env, hipStreamSynchronize(st));   // the host vectors go out of scope
+    env->py_seeded = true;
+    return SNG_OK;
+}
+
+// Orders `st` after the side stream's preparation of the streams (sng_reset), before st touches them.
+int await_prepare(SngEnv *env, hipStream_t st) {
+    if (env->prep_launched) HIP_TRY(env, hipStreamWaitEvent(st, env->prep_done, 0));
+    return SNG_OK;
 }
 
 // ... and numpy's on the device (mt_seed_kernel), queued on `st`.
@@ -634,8 +660,11 @@ int ensure_np_streams(SngEnv *env, hipStream_t st) {
         HIP_TRY(env, hipMalloc(&env->rs.pos, (size_t)env->E * sizeof(int32_t)));
     }
     if (!env->np_seeded) {
+        int rc = await_prepare(env, st);
+        if (rc) return rc;
         HIP_TRY(env, launch_ref_seed(env->rs, env->seed + (uint64_t)env->p.env_offset, env->E, st));
         env->np_seeded = true;
+        env->prepared = false;   // fresh streams: the first day prepares its blocks inline
     }
     return SNG_OK;
 }
@@ -747,10 +776,16 @@ int build_and_upload(SngEnv *env, int req_upload, hipStream_t st, bool *need_req
     return SNG_OK;
 }
 
-// After the day's planes: the PV ratios and t = 0 penalties, then the t = 0 observation.
-int finish_host_day(SngEnv *env, bool req_stream, float *obs, hipStream_t st) {
+// After the day's planes: the PV ratios and t = 0 penalties, then the t = 0 observation.  py_end / py_draw:
+// the Python streams' owed day-end draw / the ratio drawn on the device (py_ratio_kernel) over the upload.
+int finish_host_day(SngEnv *env, bool req_stream, float *obs, hipStream_t st, int py_end, int py_draw) {
     HIP_TRY(env, hipMemcpyAsync(env->ds.ratio, env->h_ratio, env->E * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipMemcpyAsync(env->ds.pen0, env->h_pen0, env->E * sizeof(double), hipMemcpyHostToDevice, st));
+    if (py_end || py_draw) {
+        int rc = await_prepare(env, st);
+        if (rc) return rc;
+        HIP_TRY(env, launch_py_ratio(env->ps, env->ds.ratio, env->E, py_end, py_draw, st));
+    }
     HIP_TRY(env, hipEventRecord(env->staging_done, st));
     env->p.req_stream = req_stream ? 1 : 0;
     env->p.packed = 0;   // word + f64 aux planes
@@ -989,9 +1024,15 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
 void sng_destroy(SngEnv *env) {
     if (!env) return;
     (void)hipSetDevice(env->device);
+    if (env->prep_stream) {
+        (void)hipStreamSynchronize(env->prep_stream);
+        (void)hipStreamDestroy(env->prep_stream);
+        (void)hipEventDestroy(env->prep_done);
+        (void)hipEventDestroy(env->day_drawn);
+    }
     DeviceState &ds = env->ds;
     void *dev[] = {ds.soc, ds.bess, ds.bess0, ds.ratio, ds.pen0, ds.word, ds.aux, ds.req, ds.flags, ds.prof,
-                   ds.episode, env->d_tables, env->rs.mt, env->rs.pos};
+                   ds.episode, env->d_tables, env->rs.mt, env->rs.pos, env->ps.mt, env->ps.pos};
     for (void *x : dev)
         if (x) (void)hipFree(x);
     void *host[] = {env->h_word, env->h_aux, env->h_req, env->h_ratio, env->h_pen0};
@@ -1019,7 +1060,7 @@ int sng_set_env_offset(SngEnv *env, int64_t offset) {
     if (!env || offset < 0) return fail(env, SNG_ERR_INVALID_ARGUMENT, "bad env offset");
     env->p.env_offset = offset;
     env->np_seeded = false;   // reference streams are re-seeded (seed + offset + i) at the next reset
-    env->py_rng.clear();
+    env->py_seeded = false;
     env->day_finished = false;
     return SNG_OK;
 }
@@ -1030,7 +1071,7 @@ int sng_set_seed(SngEnv *env, uint64_t seed, void *stream) {
     env->seed = seed;
     env->p.seed = seed;
     env->np_seeded = false;   // re-seeded (seed + offset + i) at the next reset
-    env->py_rng.clear();
+    env->py_seeded = false;
     env->day_finished = false;
     env->replays = 0;
     // device days restart at day 0 of the new streams; the loaded day stays loaded
@@ -1068,25 +1109,47 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     }
     if (rng_mode != SNG_RNG_REFERENCE) return fail(env, SNG_ERR_INVALID_ARGUMENT, "unknown rng_mode");
 
-    // the day on the device (ref_day_kernel: numpy's stream, draw for draw); the PV ratio from each
-    // env's Python stream on the host, after the day-end draw the last step still owes
+    // the day on the device (ref_day2_kernel: numpy's stream, draw for draw), then the PV ratio from each
+    // env's Python stream on the device, after the day-end draw the last step still owes
     // (smart_nanogrid_environment.py:181, 349)
-    ensure_streams(env);
     int rc = ensure_np_streams(env, st);
+    if (rc) return rc;
+    rc = ensure_py_streams(env, st);
     if (rc) return rc;
     const bool with_req = env->p.req_enabled != 0;
     if (with_req) {
         rc = ensure_req(env);
         if (rc) return rc;
     }
-    rc = ensure_staging(env, false);
+    rc = await_prepare(env, st);
     if (rc) return rc;
+    if (!env->prep_stream) {
+        HIP_TRY(env, hipStreamCreateWithFlags(&env->prep_stream, hipStreamNonBlocking));
+        HIP_TRY(env, hipEventCreateWithFlags(&env->prep_done, hipEventDisableTiming));
+        HIP_TRY(env, hipEventCreateWithFlags(&env->day_drawn, hipEventDisableTiming));
+    }
     env->p.req_stream = with_req ? 1 : 0;
-    HIP_TRY(env, launch_ref_day(env->p, env->ds, env->rs, env->E, env->i4, env->i10, env->i1, st));
-    draw_ratios(env);
-    std::fill(env->h_pen0, env->h_pen0 + env->E, 0.0);   // python index -1 of a generated day holds zeros
-    rc = finish_host_day(env, with_req, obs, st);
-    if (rc) return rc;
+    HIP_TRY(env, launch_ref_day(env->p, env->ds, env->rs, env->E, env->i4, env->i10, env->i1, !env->prepared, st));
+    HIP_TRY(env, launch_py_ratio(env->ps, env->ds.ratio, env->E, env->day_finished ? 1 : 0, 1, st));
+    env->p.packed = 0;   // word + f64 aux planes
+    env->p.req_zero = 0;
+    env->p.bump_day = 0;
+    HIP_TRY(env, sng::launch_profiles(env->p, env->ds, env->E, st));
+    // (the t = 0 penalty of a generated day is 0: observe0 writes it)
+    HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st, OBS0_GENERATED,
+                                      -1));
+    // the next day's blocks of both streams, on the side stream, while this day is stepped
+    // (mt_prepare_kernel: about every other day twists a numpy block, ~0.1 ms at 65,536 envs, off the next
+    // reset's critical path); queued behind the t = 0 observation, which it would otherwise slow down
+    HIP_TRY(env, hipEventRecord(env->day_drawn, st));
+    HIP_TRY(env, hipStreamWaitEvent(env->prep_stream, env->day_drawn, 0));
+    HIP_TRY(env, launch_mt_prepare(env->rs, env->E, env->prep_stream));
+    HIP_TRY(env, launch_mt_prepare(env->ps, env->E, env->prep_stream));
+    HIP_TRY(env, hipEventRecord(env->prep_done, env->prep_stream));
+    env->prep_launched = true;
+    env->prepared = true;
+    env->t = 0;
+    env->day_finished = false;
     env->gen_mode = SNG_RNG_REFERENCE;
     env->gen_loaded = true;
     return SNG_OK;
@@ -1110,12 +1173,11 @@ int sng_reset_replay(SngEnv *env, float *obs, void *stream) {
     if (env->gen_mode == SNG_RNG_REFERENCE) {
         // a new random_pv_shift_ratio from each env's Python stream (smart_nanogrid_environment.py:349),
         // after the day-end draw the last step still owes (:181); the numpy stream is not touched
-        ensure_streams(env);
-        int rc = ensure_staging(env, false);
+        int rc = ensure_py_streams(env, st);
         if (rc) return rc;
-        draw_ratios(env);
-        HIP_TRY(env, hipMemcpyAsync(env->ds.ratio, env->h_ratio, env->E * sizeof(double), hipMemcpyHostToDevice, st));
-        HIP_TRY(env, hipEventRecord(env->staging_done, st));
+        rc = await_prepare(env, st);
+        if (rc) return rc;
+        HIP_TRY(env, launch_py_ratio(env->ps, env->ds.ratio, env->E, env->day_finished ? 1 : 0, 1, st));
         env->p.req_zero = 1;
         env->p.bump_day = 0;
         HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, vec, st, OBS0_REPLAY, -1));
@@ -1146,9 +1208,11 @@ int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void
     // step still owes (smart_nanogrid_environment.py:181), and, when no ratio is given, the reset's own
     // draw (:349) -- what reset(generate_new_initial_values=False) consumes
     const bool draw_ratio = sc->pv_ratio == nullptr;
-    if (draw_ratio) ensure_streams(env);
-    const bool streams = !env->py_rng.empty();
-    const bool end_draw = env->day_finished && streams;
+    if (draw_ratio) {
+        rc = ensure_py_streams(env, as_stream(stream));
+        if (rc) return rc;
+    }
+    const bool end_draw = env->day_finished && env->py_seeded;
     const int N = env->p.n, V = sc->max_vehicles, S = env->slots;
     // the requested-SoC plane goes up with the chunks when the config enables it (the step reads it
     // then), else only if some penalised slot of the given days is not 1.0
@@ -1166,9 +1230,7 @@ int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void
                                         const_cast<double *>(sc->requested_soc + o),
                                         const_cast<int32_t *>(sc->arrivals + ol),
                                         const_cast<int32_t *>(sc->departures + ol), V, S};
-                              if (end_draw) (void)env->py_rng[i].py_randint(0, 180);
-                              env->h_ratio[i] = draw_ratio ? (double)env->py_rng[i].py_randint(0, 180) / 100
-                                                           : sc->pv_ratio[i];
+                              env->h_ratio[i] = draw_ratio ? 1.0 : sc->pv_ratio[i];   // (drawn on the device)
                               if (!encode_day(env->p, env->E, i, d, env->h_word, env->h_aux, env->h_req,
                                               &env->h_pen0[i], nr, e)) {
                                   e = "env " + std::to_string(i) + ": " + e;
@@ -1177,16 +1239,16 @@ int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void
                               return true;
                           });
     if (rc) {
-        // chunks before the failing env are already uploaded over the loaded day's planes and their
-        // Python-stream draws consumed: the loaded day is no longer valid, so step, replay and
-        // steps-only graphs refuse until the next reset
+        // chunks before the failing env are already uploaded over the loaded day's planes: the loaded
+        // day is no longer valid, so step, replay and steps-only graphs refuse until the next reset (no
+        // Python-stream draw was made)
         env->t = -1;
         env->gen_loaded = false;
         env->day_finished = false;
         env->err += " (the loaded day was partly overwritten: reset again)";
         return rc;
     }
-    rc = finish_host_day(env, req_enabled || need, obs, as_stream(stream));
+    rc = finish_host_day(env, req_enabled || need, obs, as_stream(stream), end_draw ? 1 : 0, draw_ratio ? 1 : 0);
     if (rc) return rc;
     env->gen_loaded = false;   // the generated day a replay restores is no longer loaded
     return SNG_OK;
@@ -1469,7 +1531,7 @@ static StateHeader state_layout(const SngEnv *env, bool with_return) {
     h.has_req = (env->ds.req && env->p.req_stream) ? 1 : 0;
     h.has_prof = env->ds.prof ? 1 : 0;
     h.has_return = with_return ? 1 : 0;
-    h.has_streams = env->py_rng.empty() ? 0 : 1;
+    h.has_streams = env->py_seeded ? 1 : 0;
     h.total_bytes = state_bytes(env, h);
     return h;
 }
@@ -1494,15 +1556,21 @@ int sng_get_state(SngEnv *env, void *buf, size_t bytes, const double *episode_re
         return e;
     };
     // the numpy streams live on the device: seeded here if no reference day drew from them yet
-    std::vector<uint32_t> np_words;
-    std::vector<int32_t> np_pos;
+    std::vector<uint32_t> np_words, py_words;
+    std::vector<int32_t> np_pos, py_pos;
     if (h.has_streams) {
         int rc = ensure_np_streams(env, st);
         if (rc) return rc;
+        rc = await_prepare(env, st);
+        if (rc) return rc;
         np_words.resize(E * 2 * kMtN);
+        py_words.resize(E * 2 * kMtN);
         np_pos.resize(E);
+        py_pos.resize(E);
         HIP_TRY(env, hipMemcpyAsync(np_words.data(), env->rs.mt, np_words.size() * 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(env, hipMemcpyAsync(np_pos.data(), env->rs.pos, E * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipMemcpyAsync(py_words.data(), env->ps.mt, py_words.size() * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipMemcpyAsync(py_pos.data(), env->ps.pos, E * 4, hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(env, hipMemcpyAsync(&h.day_counter, env->ds.episode, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
     HIP_TRY(env, pull(env->ds.soc, (size_t)env->p.n * E * 8));
@@ -1520,12 +1588,16 @@ int sng_get_state(SngEnv *env, void *buf, size_t bytes, const double *episode_re
     if (h.has_streams) {
         uint32_t *w = reinterpret_cast<uint32_t *>(out);
         for (size_t i = 0; i < E; ++i) {
-            // numpy's RandomState: the current block's 624 words and mti (sng_mt.h MT19937::save)
-            uint32_t *o = w + (2 * i) * MT19937::kStateWords;
-            const int cur = (np_pos[i] >> 16) & 1, mti = np_pos[i] & kMtPosMask;
-            std::memcpy(o, np_words.data() + (i * 2 + cur) * kMtN, kMtN * 4);
-            o[kMtN] = (uint32_t)mti;
-            env->py_rng[i].save(w + (2 * i + 1) * MT19937::kStateWords);
+            // numpy's RandomState, then Python's random: each the current block's 624 words and mti
+            // (the layout of sng_mt.h MT19937::save)
+            for (int k = 0; k < 2; ++k) {
+                const std::vector<uint32_t> &words = k ? py_words : np_words;
+                const int32_t pos = k ? py_pos[i] : np_pos[i];
+                uint32_t *o = w + (2 * i + k) * MT19937::kStateWords;
+                const int cur = (pos >> 16) & 1, mti = pos & kMtPosMask;
+                std::memcpy(o, words.data() + (i * 2 + cur) * kMtN, kMtN * 4);
+                o[kMtN] = (uint32_t)mti;
+            }
         }
     }
     std::memcpy(buf, &h, sizeof h);
@@ -1568,27 +1640,33 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
     };
     // the restored streams, checked before anything is changed: Python's into host streams, numpy's
     // into block 0 of the device streams (position = mti)
-    std::vector<MT19937> py_rng;
-    std::vector<uint32_t> np_words;
-    std::vector<int32_t> np_pos;
+    std::vector<uint32_t> np_words, py_words;
+    std::vector<int32_t> np_pos, py_pos;
     if (h.has_streams) {
         const size_t off = h.total_bytes - E * 2 * MT19937::kStateWords * 4;
         const uint32_t *w = reinterpret_cast<const uint32_t *>(static_cast<const char *>(buf) + off);
-        py_rng.resize(E);
         np_words.resize(E * kMtN);
+        py_words.resize(E * kMtN);
         np_pos.resize(E);
+        py_pos.resize(E);
         for (size_t i = 0; i < E; ++i) {
-            const uint32_t *np = w + (2 * i) * MT19937::kStateWords;
-            if (np[kMtN] > (uint32_t)kMtN + 1 || !py_rng[i].load(w + (2 * i + 1) * MT19937::kStateWords))
-                return fail(env, SNG_ERR_INVALID_ARGUMENT, "corrupt RNG stream state");
-            std::memcpy(np_words.data() + i * kMtN, np, kMtN * 4);
-            // mti = N + 1 (never seeded) cannot come from a seeded RandomState
-            np_pos[i] = (int32_t)std::min<uint32_t>(np[kMtN], (uint32_t)kMtN);
+            for (int k = 0; k < 2; ++k) {
+                const uint32_t *src = w + (2 * i + k) * MT19937::kStateWords;
+                if (src[kMtN] > (uint32_t)kMtN + 1)
+                    return fail(env, SNG_ERR_INVALID_ARGUMENT, "corrupt RNG stream state");
+                std::memcpy((k ? py_words : np_words).data() + i * kMtN, src, kMtN * 4);
+                // mti = N + 1 (never seeded) cannot come from a seeded generator
+                (k ? py_pos : np_pos)[i] = (int32_t)std::min<uint32_t>(src[kMtN], (uint32_t)kMtN);
+            }
         }
-        if (!env->rs.mt) {
-            HIP_TRY(env, hipMalloc(&env->rs.mt, E * 2 * kMtN * sizeof(uint32_t)));
-            HIP_TRY(env, hipMalloc(&env->rs.pos, E * sizeof(int32_t)));
+        for (RefStreams *r : {&env->rs, &env->ps}) {
+            if (!r->mt) {
+                HIP_TRY(env, hipMalloc(&r->mt, E * 2 * kMtN * sizeof(uint32_t)));
+                HIP_TRY(env, hipMalloc(&r->pos, E * sizeof(int32_t)));
+            }
         }
+        int rc = await_prepare(env, st);   // no preparation may still be writing the streams
+        if (rc) return rc;
     }
     HIP_TRY(env, hipMemcpyAsync(env->ds.episode, &h.day_counter, sizeof(uint64_t), hipMemcpyHostToDevice, st));
     HIP_TRY(env, push(env->ds.soc, (size_t)env->p.n * E * 8));
@@ -1606,6 +1684,9 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
         HIP_TRY(env, hipMemcpy2DAsync(env->rs.mt, 2 * kMtN * sizeof(uint32_t), np_words.data(), kMtN * sizeof(uint32_t),
                                       kMtN * sizeof(uint32_t), E, hipMemcpyHostToDevice, st));
         HIP_TRY(env, hipMemcpyAsync(env->rs.pos, np_pos.data(), E * sizeof(int32_t), hipMemcpyHostToDevice, st));
+        HIP_TRY(env, hipMemcpy2DAsync(env->ps.mt, 2 * kMtN * sizeof(uint32_t), py_words.data(), kMtN * sizeof(uint32_t),
+                                      kMtN * sizeof(uint32_t), E, hipMemcpyHostToDevice, st));
+        HIP_TRY(env, hipMemcpyAsync(env->ps.pos, py_pos.data(), E * sizeof(int32_t), hipMemcpyHostToDevice, st));
     }
     HIP_TRY(env, hipStreamSynchronize(st));
     env->seed = h.seed;
@@ -1621,7 +1702,8 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
     env->gen_loaded = h.gen_loaded != 0;
     env->replays = h.replays;
     env->np_seeded = h.has_streams != 0;
-    env->py_rng = std::move(py_rng);
+    env->py_seeded = h.has_streams != 0;
+    env->prepared = false;   // the restored position says what the next day still has to prepare
     return SNG_OK;
 }
 

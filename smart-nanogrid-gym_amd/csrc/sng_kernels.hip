@@ -33,10 +33,12 @@ constexpr int kWave = 64;
 // Streaming (nontemporal) stores for the step's bulk outputs (SoC, observations): they leave
 // less dirty L2 for the end-of-kernel release (measured 8.92 -> 8.17 us per step at 65,536 x 10).
 #define SNG_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
+#if defined(SNG_STAMPS) || defined(SNG_RD2_PROF)
+__device__ unsigned long long *g_stamps;   // diagnostic builds only: per-workgroup stamps / counters
+#endif
 #ifdef SNG_STAMPS
 // Diagnostic build only (make stamps): per-workgroup s_memrealtime stamps (100 MHz) at the
 // phase boundaries of the step kernel -> g_stamps[block*4 + k].  Never compiled into libsng.so.
-__device__ unsigned long long *g_stamps;
 #define SNG_STAMP(k)                                                                                 \
     do {                                                                                             \
         asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                  \
@@ -1465,7 +1467,7 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
             ratio = s.ratio[e];
         }
         // a generated day's python index -1 slot holds zeros; a replayed day's Requested_SOC is 0
-        if (mode != OBS0_HOST) s.pen0[e] = 0.0;
+        if (mode != OBS0_HOST) s.pen0[e] = 0.0;   // OBS0_GENERATED included
         double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
         if (p.noise) {
             const size_t plane = (size_t)(p.T + 3) * E;
@@ -1525,7 +1527,7 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
     }
     // a host day: profile_kernel read the counter for this day's factors, so the next day draws the
     // next value (a device day's counter is advanced by its first step; a replay keeps its day's)
-    if (mode == OBS0_HOST && blockIdx.x == 0 && tid == 0) *s.episode += 1;
+    if ((mode == OBS0_HOST || mode == OBS0_GENERATED) && blockIdx.x == 0 && tid == 0) *s.episode += 1;
     __syncthreads();
     copy_out<BLOCK>(obs + e0 * O, lds, nblk * O, vec_io != 0, tid);
 }
@@ -1956,7 +1958,7 @@ static void launch_step_n(const Params &p, const DeviceState &s, const InfoPtrs 
     }
 }
 
-#ifdef SNG_STAMPS
+#if defined(SNG_STAMPS) || defined(SNG_RD2_PROF)
 extern "C" int sng_debug_set_stamps(unsigned long long *dev_ptr) {
     return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -1;
 }
@@ -2188,6 +2190,11 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
 // slot of block k - 2, which the ring has consumed by then (it runs at most 128 words ahead).
 // LDS layout ring[slot][lane]: lanes reading any slots hit distinct banks.
 constexpr int kRing = 128;
+// RandomState.random_sample from two tempered words (numpy's rk_double: 53 bits, a >> 5 and b >> 6)
+__device__ __forceinline__ double rand53(uint32_t wa, uint32_t wb) {
+    const int32_t a = (int32_t)(wa >> 5), b = (int32_t)(wb >> 6);
+    return (a * 67108864.0 + b) / 9007199254740992.0;
+}
 // Envs per wavefront (lanes >= kRefEnvs mirror lane % kRefEnvs: same stream, same branches, nothing
 // stored).  64 at 65,536 envs: 32 / 16 / 8 envs per wavefront ran the day in 338 / 405 / 505 us against
 // 331 us (rocprof, one box) -- the kernel is bound by the instructions the divergent wavefronts issue,
@@ -2196,13 +2203,18 @@ constexpr int kRing = 128;
 #define SNG_REF_ENVS 64
 #endif
 constexpr int kRefEnvs = SNG_REF_ENVS;
-struct MtRing {
+template <int ENVS>
+struct MtRingT {
     uint32_t *blk;
-    uint32_t *ring;   // this lane's ring: ring[slot * kRefEnvs], slot < kRing
+    uint32_t *ring;   // this lane's ring: ring[slot * ENVS], slot < kRing
     int cur0;
     int head, tail;   // stream words (from the current block's start) drawn / loaded into the ring
     int q0;           // the day's first word (mti at the start)
     int avail;        // stream blocks materialised: 0 .. avail - 1
+#ifdef SNG_RD2_PROF
+    unsigned long long prof_refill = 0;
+    unsigned prof_nrefill = 0, prof_dry = 0;
+#endif
     __device__ __forceinline__ const uint32_t *word_ptr(int q) const {
         const int k = q / kMtN;
         return blk + ((cur0 + k) & 1) * kMtN + (q - k * kMtN);
@@ -2216,16 +2228,33 @@ struct MtRing {
     }
     // wave-uniform: lanes holding <= 64 words load the next 64 (tail stays a multiple of 4)
     __device__ __forceinline__ void refill() {
+#ifdef SNG_RD2_PROF
+        const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
+        ++prof_nrefill;
+#endif
+        refill_();
+#ifdef SNG_RD2_PROF
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        prof_refill += __builtin_amdgcn_s_memtime() - t0_;
+#endif
+    }
+    __device__ __forceinline__ void refill_() {
         if (tail - head <= kRing / 2) {
             materialise(tail + kRing / 2 - 1);
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             u32x4 x[kRing / 8];
+            // the 64 words span at most two blocks: word q = tail + 4g is in block k0 up to offset 624
+            const int k0 = tail / kMtN, off0 = tail - k0 * kMtN;
+            const uint32_t *b0 = blk + ((cur0 + k0) & 1) * kMtN, *b1 = blk + ((cur0 + k0 + 1) & 1) * kMtN;
 #pragma unroll
-            for (int g = 0; g < kRing / 8; ++g) x[g] = *reinterpret_cast<const u32x4 *>(word_ptr(tail + 4 * g));
+            for (int g = 0; g < kRing / 8; ++g) {
+                const int off = off0 + 4 * g;
+                x[g] = *reinterpret_cast<const u32x4 *>(off < kMtN ? b0 + off : b1 + (off - kMtN));
+            }
 #pragma unroll
             for (int g = 0; g < kRing / 8; ++g)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ring[((tail + 4 * g + i) & (kRing - 1)) * kRefEnvs] = x[g][i];
+                for (int i = 0; i < 4; ++i) ring[((tail + 4 * g + i) & (kRing - 1)) * ENVS] = mt_temper(x[g][i]);
             tail += kRing / 2;
         }
     }
@@ -2234,21 +2263,27 @@ struct MtRing {
     }
     __device__ __forceinline__ uint32_t next() {
         if (head >= tail) {   // the ring ran dry inside one step: the word's aligned group straight in
+#ifdef SNG_RD2_PROF
+            ++prof_dry;
+#endif
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             materialise(head);
             const int g = head & ~3;
             const u32x4 x = *reinterpret_cast<const u32x4 *>(word_ptr(g));
 #pragma unroll
-            for (int i = 0; i < 4; ++i) ring[((g + i) & (kRing - 1)) * kRefEnvs] = x[i];
+            for (int i = 0; i < 4; ++i) ring[((g + i) & (kRing - 1)) * ENVS] = mt_temper(x[i]);
             tail = g + 4;
         }
-        const uint32_t y = ring[(head & (kRing - 1)) * kRefEnvs];
+        const uint32_t y = ring[(head & (kRing - 1)) * ENVS];
         ++head;
-        return mt_temper(y);
+        return y;
     }
+    // word head + k, without advancing: valid for k < kPeek after a top_up (every lane then holds more
+    // than kRing / 4 words)
+    __device__ __forceinline__ uint32_t peek(int k) const { return ring[((head + k) & (kRing - 1)) * ENVS]; }
     __device__ __forceinline__ double random() {
-        const int32_t a = (int32_t)(next() >> 5), b = (int32_t)(next() >> 6);
-        return (a * 67108864.0 + b) / 9007199254740992.0;
+        const uint32_t a = next();
+        return rand53(a, next());
     }
     __device__ __forceinline__ double uniform(double lo, double hi) { return lo + (hi - lo) * random(); }
     // a draw whose value is discarded (a uniform: two words) only advances the stream
@@ -2283,6 +2318,7 @@ struct MtRing {
         return (((cur0 + k) & 1) << 16) | (k + 1 < avail ? kMtNextReady : 0) | (head - k * kMtN);
     }
 };
+using MtRing = MtRingT<kRefEnvs>;
 
 // The day of every env: generate_day + encode_day (sng_api.cpp) on one thread per env, charger by
 // charger; the lanes of a wavefront step (charger, t) together, so the timeline stores coalesce.
@@ -2361,6 +2397,279 @@ __global__ __launch_bounds__(kRefBlock) void ref_day_kernel(Params p, DeviceStat
     if (live) rs.pos[e] = rng.position();
 }
 
+// The same day in two phases per charger, as generate_kernel draws a device day: (1) the charger's
+// vehicles, visiting only the steps that draw (a free step draws the arrival test, an arrival the
+// vehicle's values; an occupied step and a departure step draw nothing, charging_station.py:200-279),
+// into a per-lane list in LDS; (2) the word / f64 aux (/ req) timeline from the list, branch-free, step
+// by step.  The steps-major loop above executed the arrival path under a mask in nearly every (charger,
+// step) iteration of a wavefront; here a wavefront iterates once per draw step of its busiest lane
+// (about 5 of a charger's 24 steps draw).  The stream is consumed draw for draw as above.
+constexpr int kRefVeh = 8;   // vehicles per charger-day (T / (4/dt + 1) + 1 <= 7 for every dt dividing 24 h) + sentinel
+// Phase 1 reads each draw step's words from the ring in two batches of LDS reads instead of one round
+// trip per word: after a top_up every lane still drawing holds more than kRing / 4 words, so the 10 words
+// an arrival may need first (arrival test, SoC, the discarded uniform, four capacity candidates) and the
+// 6 it may need next (requested SoC, four departure candidates) are peeked without a bound check.  A
+// masked rejection (numpy's legacy bounded randint) takes the first of four candidates that passes; all
+// four rejected (p < 0.2 % for a capacity, < 0.4 % for a departure) continues word by word.
+// A step without a vehicle draws only its arrival test, so phase 1 tests the next kScan steps together
+// (integer compares, arrives()) and takes the first arrival with its vehicle in the same iteration: a
+// wavefront iterates ~5 times per charger-day instead of once per drawing step of its busiest lane (~15).
+constexpr int kScan = 4;
+// round(random.rand() - 0.1) == 1 (charging_station.py:214-215) on the 53-bit draw K = (a >> 5) << 26 |
+// (b >> 6), random.rand() = K / 2^53 (rk_double): fl(K / 2^53 - 0.1) > 0.5 is monotone in K and holds
+// from K = 0x13333333333334 on (checked against the double expression at every K within 3,000 of it and
+// at 10^5 random K; tests/test_ref_arrival_threshold.py)
+constexpr uint64_t kArrive53 = 0x13333333333334ull;
+__device__ __forceinline__ bool arrives(uint32_t wa, uint32_t wb) {
+    return ((((uint64_t)(wa >> 5)) << 26) | (uint64_t)(wb >> 6)) >= kArrive53;
+}
+template <int TT, bool REQ, int ENVS>
+__global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceState s, RefStreams rs, int64_t E,
+                                                             int i4, int i10, int i1) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t rd_lds[];
+    uint32_t *rings = rd_lds;                                          // [kRing][ENVS]
+    uint32_t *s_veh = rings + kRing * ENVS;                         // [V][ENVS] ta | cap << 8 | dep << 16
+    double *s_soc = reinterpret_cast<double *>(s_veh + kRefVeh * ENVS);   // [V][ENVS] arrival SoC
+    double *s_req = s_soc + kRefVeh * ENVS;                          // [V][ENVS] requested SoC (REQ)
+    const int lane = threadIdx.x % ENVS;   // the env slot; lanes >= ENVS mirror it
+    const int64_t e0 = (int64_t)blockIdx.x * ENVS;
+    const bool live = e0 + lane < E && (int)threadIdx.x < ENVS;
+    const int64_t e = e0 + lane < E ? e0 + lane : E - 1;   // past E: env E - 1's stream, nothing stored
+    const int32_t pos = rs.pos[e];
+    const int mti = pos & kMtPosMask;
+    MtRingT<ENVS> rng{rs.mt + (size_t)e * 2 * kMtN, rings + lane, (pos >> 16) & 1, mti, mti & ~3, mti, 2};
+    const int T = TT > 0 ? TT : p.T, n = p.n;
+    const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;   // as generate_kernel
+    const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
+                              : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
+    const uint32_t el8 = (uint32_t)e * 8u;
+    const size_t nE = (size_t)n * (size_t)E;
+#ifdef SNG_RD2_PROF
+    const unsigned long long k_start = __builtin_amdgcn_s_memrealtime();
+    unsigned long long acc1 = 0, acc2 = 0;
+    unsigned iters = 0;
+#endif
+    for (int c = 0; c < n; ++c) {
+        const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
+#ifdef SNG_RD2_PROF
+        const unsigned long long p1 = __builtin_amdgcn_s_memtime();
+#endif
+        // phase 1: the charger's vehicles, one iteration per step that draws
+        int t = 0, nv = 0;
+#ifdef SNG_RD2_NOPH1   // diagnostic builds only: fake vehicles, no stream draws
+        for (; t < T && nv < kRefVeh - 1; ++nv) {
+            s_veh[nv * ENVS + lane] = (uint32_t)t | (40u << W_CAP_SHIFT) | ((uint32_t)(t + i4 + (lane & 3)) << W_DEP_SHIFT);
+            s_soc[nv * ENVS + lane] = 0.5;
+            t = t + i4 + (lane & 3) + 2;
+        }
+        t = T;
+#endif
+        while (t < T) {
+#ifdef SNG_RD2_PROF
+            ++iters;
+#endif
+            rng.top_up();   // ballots over the lanes still drawing: each then holds > kRing / 4 words
+            // the next kScan steps' arrival draws at once: the first that arrives, the free steps before
+            // it consumed together
+            uint32_t a[2 * kScan];
+#pragma unroll
+            for (int k = 0; k < 2 * kScan; ++k) a[k] = rng.peek(k);
+            int j = kScan;
+#pragma unroll
+            for (int kk = kScan - 1; kk >= 0; --kk) j = arrives(a[2 * kk], a[2 * kk + 1]) ? kk : j;
+            const int skip = min(j, T - t);
+            rng.head += 2 * skip;
+            t += skip;
+            if (t < T && j < kScan) {   // an arrival at step t
+                uint32_t w[10];   // from the arrival draw: w[0], w[1] are it (not reread)
+#pragma unroll
+                for (int k = 2; k < 10; ++k) w[k] = rng.peek(k);
+                const double soc = 0.1 + (0.9 - 0.1) * rand53(w[2], w[3]);      // uniform(0.1, 0.9), :257-259
+                const double lo = soc <= 0.9 ? soc + 0.1 : 1.0;
+                // w[4], w[5]: the discarded uniform (:219)
+                uint32_t cap = 40u;
+                bool seq = false;   // the draws continue word by word (a rejection streak)
+                if (p.diff_caps) {   // randint(15, 120) (:267-269): mask 127, accept <= 104
+                    int k = 4;
+                    uint32_t cv = 0u;
+#pragma unroll
+                    for (int kk = 3; kk >= 0; --kk) {   // the first candidate that passes, without an index
+                        const uint32_t x = w[6 + kk] & 127u;
+                        k = (x <= 104u) ? kk : k;
+                        cv = (x <= 104u) ? x : cv;
+                    }
+                    if (k < 4) {
+                        cap = 15u + cv;
+                        rng.head += 7 + k;
+                    } else {
+                        rng.head += 10;
+                        cap = (uint32_t)rng.randint(15, 120);
+                        seq = true;
+                    }
+                } else {
+                    rng.head += 6;
+                }
+                double rq = 1.0;
+                const int high = min(t + i10, T + i1), low = t + i4;             // :271-279
+                int dep = low;
+                if (!seq) {
+                    uint32_t v[6];
+#pragma unroll
+                    for (int k = 0; k < 6; ++k) v[k] = rng.peek(k);
+                    constexpr int U = REQ ? 2 : 0;
+                    if (REQ) rq = lo + (1.0 - lo) * rand53(v[0], v[1]);       // uniform(lo, 1), :261-265
+                    int used = U;
+                    if (low < high && high - 1 - low > 0) {   // randint(low, high); one value draws nothing
+                        const uint32_t span = (uint32_t)(high - 1 - low);
+                        uint32_t mask = span;
+                        mask |= mask >> 1;
+                        mask |= mask >> 2;
+                        mask |= mask >> 4;
+                        mask |= mask >> 8;
+                        mask |= mask >> 16;
+                        int k = 4;
+                        uint32_t dv = 0u;
+#pragma unroll
+                        for (int kk = 3; kk >= 0; --kk) {
+                            const uint32_t x = v[U + kk] & mask;
+                            k = (x <= span) ? kk : k;
+                            dv = (x <= span) ? x : dv;
+                        }
+                        if (k < 4) {
+                            dep = low + (int)dv;
+                            used += k + 1;
+                        } else {
+                            rng.head += U + 4;
+                            used = 0;
+                            uint32_t x;
+                            while ((x = (rng.next() & mask)) > span) {
+                            }
+                            dep = low + (int)x;
+                        }
+                    }
+                    rng.head += used;
+                } else {
+                    rq = REQ ? rng.uniform(lo, 1.0) : 1.0;
+                    dep = (low >= high) ? low : rng.randint(low, high);
+                }
+                const int vi = nv < kRefVeh - 1 ? nv : kRefVeh - 2;   // at most 7 (see kRefVeh)
+                s_veh[vi * ENVS + lane] = (uint32_t)t | (cap << W_CAP_SHIFT) | ((uint32_t)dep << W_DEP_SHIFT);
+                s_soc[vi * ENVS + lane] = soc;
+                if (REQ) s_req[vi * ENVS + lane] = rq;
+                nv = vi + 1;
+                t = dep + 1;   // occupied until dep - 1; the departure step is empty and draws nothing
+            }
+        }
+        s_veh[nv * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);   // sentinel: never arrives
+        s_veh[(nv + 1 < kRefVeh ? nv + 1 : nv) * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);
+#ifdef SNG_RD2_PROF
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        const unsigned long long p2 = __builtin_amdgcn_s_memtime();
+        acc1 += p2 - p1;
+#endif
+        // phase 2: the timeline (encode_day, sng_api.cpp): cur = the vehicle of step t until step t has
+        // passed its departure step, nxt the one after it (read a step ahead); a stay of zero steps
+        // (dep == arrival, possible when 4/dt < 1) still marks its arrival step STATIC, as the host
+        // encoder's arrival list does
+        int v = 0;
+        uint32_t cur = s_veh[lane], nxt = s_veh[ENVS + lane];
+        double soc_cur = s_soc[lane], soc_nxt = s_soc[ENVS + lane];
+        double req_cur = REQ ? s_req[lane] : 1.0, req_nxt = REQ ? s_req[ENVS + lane] : 1.0;
+        bool prev_occ = false;
+        uint32_t prev_rem = 0u;
+        double prev_req = 0.0;
+#pragma unroll
+        for (int tt = 0; tt < T; ++tt) {
+            const uint32_t ta = cur & 0xffu, dep = cur >> W_DEP_SHIFT;
+            const bool adv = (uint32_t)(tt + 1) > dep;   // step t + 1 belongs to the next vehicle
+            const int vr = v + 2 < kRefVeh ? v + 2 : kRefVeh - 1;
+            const uint32_t nn = s_veh[vr * ENVS + lane];   // list[v + 2], for when nxt becomes current
+            const double soc_nn = s_soc[vr * ENVS + lane];
+            const double req_nn = REQ ? s_req[vr * ENVS + lane] : 1.0;
+            const bool occ = (uint32_t)tt >= ta && (uint32_t)tt < dep;
+            const bool arrived = (uint32_t)tt == ta;
+            const bool running = !arrived && prev_occ;
+            const uint32_t rem = occ ? dep - (uint32_t)tt : 0u;
+            const bool pen = prev_rem - pen_lo <= pen_span;   // prev_rem = 0: empty at t-1
+            const size_t plane = (size_t)tt * nE;
+#ifdef SNG_RD2_NOSTORE   // diagnostic builds only: the day's draws without its timeline stores
+            if (live && soc_cur == 12345.0) {
+#else
+            // every lane stores: a lane that is not live mirrors a live one (the same env's stream, so
+            // the same values to the same addresses), and straight-line stores let the compiler count
+            // them in vmcnt instead of draining them before the next refill's words are read
+            {
+#endif
+                // plain global stores (a uniform plane pointer + the env): one buffer descriptor per plane
+                // would not fit the SGPRs of the unrolled walk
+                const size_t row = plane + (size_t)c * (size_t)E;
+                s.word[row + (size_t)e] = pack_word(occ, !running, pen, occ ? (cur >> W_CAP_SHIFT) & 0xffu : 0u, rem);
+                s.aux[row + (size_t)e] = (occ && !running) ? soc_cur : 0.0;
+                if (REQ && tt > 0) s.req[row + (size_t)e] = prev_req;   // Requested_SOC[c, t-1]
+            }
+            prev_occ = occ;
+            prev_rem = rem;
+            prev_req = occ ? req_cur : 0.0;
+            v += adv ? 1 : 0;
+            cur = adv ? nxt : cur;
+            soc_cur = adv ? soc_nxt : soc_cur;
+            req_cur = adv ? req_nxt : req_cur;
+            nxt = adv ? nn : nxt;
+            soc_nxt = adv ? soc_nn : soc_nxt;
+            req_nxt = adv ? req_nn : req_nxt;
+        }
+        if (REQ) bst(s.req, el8, prev_req, r8);   // slot 0: Requested_SOC[c, T-1]
+#ifdef SNG_RD2_PROF
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        acc2 += __builtin_amdgcn_s_memtime() - p2;
+#endif
+    }
+    if (live) rs.pos[e] = rng.position();
+#ifdef SNG_RD2_PROF
+    const unsigned long long k_end = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0 && g_stamps) {
+        unsigned long long *o = g_stamps + (size_t)blockIdx.x * 8;
+        o[0] = k_start;
+        o[1] = k_end;
+        o[2] = acc1;
+        o[3] = acc2;
+        o[4] = rng.prof_refill;
+        o[5] = rng.prof_nrefill;
+        o[6] = iters;
+    }
+    const unsigned dry = rng.prof_dry;
+    if (g_stamps && dry) atomicAdd(g_stamps + (size_t)blockIdx.x * 8 + 7, (unsigned long long)dry);
+#endif
+}
+
+__host__ __device__ constexpr size_t ref_day2_lds_bytes(bool req, int envs) {
+    return (size_t)kRing * envs * 4 + (size_t)kRefVeh * envs * (4 + 8 + (req ? 8 : 0));
+}
+
+#ifndef SNG_REF2_ENVS
+#define SNG_REF2_ENVS 0   // 0: by population size (ref_day2_envs); A/B builds fix it
+#endif
+// Envs per wavefront of ref_day2_kernel: each wavefront's day is one serial chain (an env's stream is
+// consumed charger after charger), so small populations spread over more, thinner wavefronts.
+static int ref_day2_envs(int64_t E) {
+    if (SNG_REF2_ENVS) return SNG_REF2_ENVS;
+    return E >= 65536 ? 64 : E >= 16384 ? 32 : E >= 4096 ? 16 : 8;
+}
+
+template <int TT, bool REQ>
+static void launch_ref_day2(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
+                            int i1, hipStream_t stream) {
+    const int envs = ref_day2_envs(E);
+    const dim3 grid((unsigned)((E + envs - 1) / envs)), block(kRefBlock);
+    const size_t lds = ref_day2_lds_bytes(REQ, envs);
+    switch (envs) {
+        case 8: hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, 8>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
+        case 16: hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, 16>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
+        case 32: hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, 32>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
+        default: hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, 64>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
+    }
+}
+
 hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream) {
     hipLaunchKernelGGL(mt_seed_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, rs, seed0, E);
     return hipGetLastError();
@@ -2368,13 +2677,77 @@ hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipS
 
 // One reference-RNG day of every env into the word / aux (/ req) planes; ratio, pen0 and the t = 0
 // observation are the caller's (the Python stream stays on the host).
-hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
-                          int i1, hipStream_t stream) {
+hipError_t launch_mt_prepare(const RefStreams &rs, int64_t E, hipStream_t stream) {
     hipLaunchKernelGGL(mt_prepare_kernel, dim3((unsigned)((E + 3) / 4)), dim3(256), 0, stream, rs, E);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ref_day_kernel, dim3((unsigned)((E + kRefEnvs - 1) / kRefEnvs)), dim3(kRefBlock), 0, stream, p,
-                       s, rs, E, i4, i10, i1);
+    return hipGetLastError();
+}
+
+// prepare = false: the streams' blocks were prepared for this day already (sng_api.cpp prepares the next
+// day's on a side stream while a day is stepped)
+hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
+                          int i1, bool prepare, hipStream_t stream) {
+    if (prepare) {
+        hipError_t e = launch_mt_prepare(rs, E, stream);
+        if (e != hipSuccess) return e;
+    }
+#ifdef SNG_REF_STEPS   // A/B builds: the steps-major kernel
+    const dim3 grid((unsigned)((E + kRefEnvs - 1) / kRefEnvs)), block(kRefBlock);
+    hipLaunchKernelGGL(ref_day_kernel, grid, block, 0, stream, p, s, rs, E, i4, i10, i1);
+#else
+    const bool req = p.req_stream != 0;
+    if (p.T == 24) {
+        if (req) launch_ref_day2<24, true>(p, s, rs, E, i4, i10, i1, stream);
+        else launch_ref_day2<24, false>(p, s, rs, E, i4, i10, i1, stream);
+    } else {
+        if (req) launch_ref_day2<0, true>(p, s, rs, E, i4, i10, i1, stream);
+        else launch_ref_day2<0, false>(p, s, rs, E, i4, i10, i1, stream);
+    }
+#endif
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// The reference's Python `random` stream of every env on the device (random.seed(seed + global env),
+// CPython's MT19937; seeded on the host with init_by_array, sng_mt.h, and uploaded once): the PV ratio
+// random.randint(0, 180) / 100 of a reset (smart_nanogrid_environment.py:349), after the day-end draw
+// the last step still owes (:181).  RefStreams layout (two blocks per env, mt_prepare_kernel keeps the
+// successor ready); a block boundary without a ready successor is twisted on the lane.
+// Thread = env.  end_draw: consume the owed day-end randint first; draw: write ratio[e].
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void py_ratio_kernel(RefStreams ps, double *__restrict__ ratio, int64_t E,
+                                                       int end_draw, int draw) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e >= E) return;
+    uint32_t *blk = ps.mt + (size_t)e * 2 * kMtN;
+    const int32_t pos = ps.pos[e];
+    int cur = (pos >> 16) & 1, mti = pos & kMtPosMask;
+    bool ready = (pos & kMtNextReady) != 0;
+    auto next = [&]() -> uint32_t {
+        if (mti >= kMtN) {
+            if (!ready) mt_twist_lane(blk + cur * kMtN, blk + (cur ^ 1) * kMtN);
+            cur ^= 1;
+            mti -= kMtN;
+            ready = false;
+        }
+        return mt_temper(blk[cur * kMtN + mti++]);
+    };
+    auto randint180 = [&]() -> int {   // random.randint(0, 180): _randbelow(181), getrandbits(8) rejection
+        uint32_t r;
+        do {
+            r = next() >> 24;
+        } while (r >= 181u);
+        return (int)r;
+    };
+    if (end_draw) (void)randint180();
+    if (draw) ratio[e] = (double)randint180() / 100;
+    ps.pos[e] = (cur << 16) | (ready ? kMtNextReady : 0) | mti;
+}
+
+hipError_t launch_py_ratio(const RefStreams &ps, double *ratio, int64_t E, int end_draw, int draw,
+                           hipStream_t stream) {
+    if (!end_draw && !draw) return hipSuccess;
+    hipLaunchKernelGGL(py_ratio_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, ps, ratio, E,
+                       end_draw, draw);
     return hipGetLastError();
 }
 

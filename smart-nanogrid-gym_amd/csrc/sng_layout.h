@@ -149,6 +149,8 @@ enum Obs0Mode : int32_t {
                        // (profile_kernel read it for this day's profile factors)
     OBS0_DEVICE = 1,   // device-RNG day of a wide station (generator launched without its t = 0 blocks):
                        // ratio drawn from the day's stream, pen0 = 0; the day's first step advances the counter
+    OBS0_GENERATED = 3,   // reference-RNG day generated on the device: ratio uploaded, pen0 = 0 (a generated
+                          // day's python index -1 slot holds zeros); advances the day counter like OBS0_HOST
     OBS0_REPLAY = 2,   // replayed day, reset(generate_new_initial_values=False): pen0 = 0, counter untouched;
                        // ratio uploaded (reference RNG) or drawn from the replay stream (device RNG)
 };

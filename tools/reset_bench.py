@@ -5,8 +5,9 @@ the VecEnv default rng='reference' (vec_env.py step_wait).
 
     python tools/reset_bench.py [--envs 4096 65536] [--repeats 5]
 
-Prints one JSON line per size: host-wall ms per reset (reset call + stream sync) for reference-RNG,
-device-RNG and replay resets, the host threads used, and the GPU-only day for comparison.
+Prints one JSON line per size: host-wall ms per reset (reset call + stream sync) for reference-RNG
+resets after a stepped day (as SB3's automatic reset follows a day) and back to back, device-RNG and
+replay resets, and the host threads used.
 """
 import argparse
 import json
@@ -24,13 +25,20 @@ from smart_nanogrid_gym import SmartNanogridVecEnv  # noqa: E402
 from smart_nanogrid_gym._native import lib  # noqa: E402
 
 
-def timed(fn, repeats, sync=True):
+def timed(fn, repeats, sync=True, between=None):
+    """Host-wall ms of fn(); between(), untimed, runs before each repetition.  sync=True waits for the
+    whole device (work the call left on side streams included), "stream" for the caller's stream only (what
+    the next step_tensors is ordered after), False for nothing (the host call alone)."""
     out = []
     for _ in range(repeats):
+        if between is not None:
+            between()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         fn()
-        if sync:
+        if sync == "stream":
+            torch.cuda.current_stream().synchronize()
+        elif sync:
             torch.cuda.synchronize()
         out.append((time.perf_counter() - t0) * 1e3)
     torch.cuda.synchronize()
@@ -41,7 +49,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, nargs="+", default=[4096, 65536])
     ap.add_argument("--chargers", type=int, default=10)
-    ap.add_argument("--repeats", type=int, default=5)
+    ap.add_argument("--repeats", type=int, default=9)
     args = ap.parse_args()
     kw = dict(number_of_chargers=args.chargers, time_interval="1h", charging_mode="bounded",
               vehicle_uncharged_penalty_mode="sparse")
@@ -50,9 +58,24 @@ def main():
         v.reset_tensors()   # first call: allocates streams and pinned staging
         zero = torch.zeros((E, v.act_dim), device=v.device)
 
+        def day():   # the day a reset follows (SB3's automatic reset comes after the last step)
+            for t in range(v.timesteps):
+                v.step_tensors(zero)
+
         res = {"envs": E, "chargers": args.chargers, "host_threads": int(lib().sng_host_threads()),
-               "reference_reset": timed(lambda: v.reset_tensors(rng="reference"), args.repeats),
+               # after a stepped day: the next day's stream blocks were prepared while it was stepped
+               "reference_reset": timed(lambda: v.reset_tensors(rng="reference"), args.repeats, between=day),
+               # the same, until the observations are ready on the caller's stream (the next day's stream
+               # blocks are still being prepared on the side stream, overlapping the day's steps)
+               "reference_reset_stream_sync": timed(lambda: v.reset_tensors(rng="reference"), args.repeats,
+                                                    sync="stream", between=day),
+               # resets back to back: the preparation of each day's blocks waits on the critical path
+               "reference_reset_back_to_back": timed(lambda: v.reset_tensors(rng="reference"), args.repeats),
                "device_reset": timed(lambda: v.reset_tensors(rng="device"), args.repeats)}
+        # a whole reference-RNG day (reset + its steps), device-synced: the side-stream preparation
+        # overlaps the steps
+        res["reference_day"] = timed(lambda: (v.reset_tensors(rng="reference"), day()), args.repeats)
+        res["device_day"] = timed(lambda: (v.reset_tensors(rng="device"), day()), args.repeats)
         v.reset_tensors(rng="reference")
         for t in range(v.timesteps):
             v.step_tensors(zero)
