@@ -633,7 +633,7 @@ int ensure_py_streams(SngEnv *env, hipStream_t st) {
         for (int64_t i = b; i < en; ++i) {
             m.seed_python(s0 + (uint64_t)i);
             m.save(st_words);
-            std::memcpy(words.data() + (size_t)i * kMtN, st_words, kMtN * sizeof(uint32_t));
+            for (int k = 0; k < kMtN; ++k) words[(size_t)i * kMtN + k] = mt_temper_word(st_words[k]);   // RefStreams keep tempered words
             pos[i] = (int32_t)st_words[kMtN];   // block 0, mti = N
         }
     });
@@ -1595,7 +1595,8 @@ int sng_get_state(SngEnv *env, void *buf, size_t bytes, const double *episode_re
                 const int32_t pos = k ? py_pos[i] : np_pos[i];
                 uint32_t *o = w + (2 * i + k) * MT19937::kStateWords;
                 const int cur = (pos >> 16) & 1, mti = pos & kMtPosMask;
-                std::memcpy(o, words.data() + (i * 2 + cur) * kMtN, kMtN * 4);
+                const uint32_t *src = words.data() + (i * 2 + cur) * kMtN;
+                for (int k = 0; k < kMtN; ++k) o[k] = mt_untemper_word(src[k]);   // the raw state
                 o[kMtN] = (uint32_t)mti;
             }
         }
@@ -1654,7 +1655,8 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
                 const uint32_t *src = w + (2 * i + k) * MT19937::kStateWords;
                 if (src[kMtN] > (uint32_t)kMtN + 1)
                     return fail(env, SNG_ERR_INVALID_ARGUMENT, "corrupt RNG stream state");
-                std::memcpy((k ? py_words : np_words).data() + i * kMtN, src, kMtN * 4);
+                uint32_t *dst = (k ? py_words : np_words).data() + i * kMtN;
+                for (int q = 0; q < kMtN; ++q) dst[q] = mt_temper_word(src[q]);   // RefStreams keep tempered words
                 // mti = N + 1 (never seeded) cannot come from a seeded generator
                 (k ? py_pos : np_pos)[i] = (int32_t)std::min<uint32_t>(src[kMtN], (uint32_t)kMtN);
             }

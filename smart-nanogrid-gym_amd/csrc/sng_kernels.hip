@@ -2088,13 +2088,8 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
 //                      twist's three dependent ranges, 64 words at a time, in LDS)
 //   ref_day_kernel     per env, one thread: the day's draws and its timeline
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
-    y ^= y >> 11;
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
-    y ^= y >> 18;
-    return y;
-}
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) { return mt_temper_word(y); }
+__device__ __forceinline__ uint32_t mt_untemper(uint32_t y) { return mt_untemper_word(y); }
 
 __device__ __forceinline__ uint32_t mt_mix(uint32_t a, uint32_t b) {   // twist term of words kk, kk + 1
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
@@ -2118,11 +2113,14 @@ __device__ __forceinline__ void mt_twist_wave(const uint32_t *A, uint32_t *B, in
 
 // the same by one thread, in place of the stream's exhausted other block (a day that draws past two
 // blocks: not reachable by the generator's draw counts, kept for completeness)
+// (both blocks tempered, as the streams keep them)
 __device__ __noinline__ void mt_twist_lane(const uint32_t *A, uint32_t *B) {
     constexpr int NM = kMtN - kMtM;
-    for (int k = 0; k < NM; ++k) B[k] = A[k + kMtM] ^ mt_mix(A[k], A[k + 1]);
-    for (int k = NM; k < kMtN - 1; ++k) B[k] = B[k - NM] ^ mt_mix(A[k], A[k + 1]);
-    B[kMtN - 1] = B[kMtM - 1] ^ mt_mix(A[kMtN - 1], B[0]);
+    auto a = [&](int k) { return mt_untemper(A[k]); };
+    auto b = [&](int k) { return mt_untemper(B[k]); };
+    for (int k = 0; k < NM; ++k) B[k] = mt_temper(a(k + kMtM) ^ mt_mix(a(k), a(k + 1)));
+    for (int k = NM; k < kMtN - 1; ++k) B[k] = mt_temper(b(k - NM) ^ mt_mix(a(k), a(k + 1)));
+    B[kMtN - 1] = mt_temper(b(kMtM - 1) ^ mt_mix(a(kMtN - 1), b(0)));
 }
 
 // np.random.seed(s): init_genrand(s & 0xffffffff); mti = N, so the first draw twists
@@ -2131,10 +2129,10 @@ __global__ __launch_bounds__(256) void mt_seed_kernel(RefStreams rs, uint64_t se
     if (e >= E) return;
     uint32_t *b = rs.mt + (size_t)e * 2 * kMtN;
     uint32_t x = (uint32_t)(seed0 + (uint64_t)e);
-    b[0] = x;
+    b[0] = mt_temper(x);
     for (int i = 1; i < kMtN; ++i) {
         x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)i;
-        b[i] = x;
+        b[i] = mt_temper(x);
     }
     rs.pos[e] = kMtN;   // block 0, mti = N
 }
@@ -2144,7 +2142,7 @@ __global__ __launch_bounds__(256) void mt_seed_kernel(RefStreams rs, uint64_t se
 // position word is cur << 16 | kMtNextReady | mti; kMtNextReady says the other slot already holds the
 // current block's successor (a day of ~300 draws leaves it untouched), so most days need no twist here.
 __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t E) {
-    __shared__ uint32_t lds[4][2][kMtN];
+    __shared__ __attribute__((aligned(16))) uint32_t lds[4][2][kMtN];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const int64_t e = (int64_t)blockIdx.x * 4 + wave;
     if (e >= E) return;   // wave-uniform
@@ -2158,7 +2156,25 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
         cur ^= 1;
         mti -= kMtN;
     }
-    for (int k = lane; k < kMtN; k += kWave) A[k] = blk[cur * kMtN + k];
+    // 16 B per lane: a block is 156 groups of 4 words
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    auto load_block = [&](int slot, uint32_t *dst) {
+        for (int g = lane; g < kMtN / 4; g += kWave) {
+            u32x4 x = *reinterpret_cast<const u32x4 *>(blk + slot * kMtN + 4 * g);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = mt_untemper(x[i]);
+            *reinterpret_cast<u32x4 *>(dst + 4 * g) = x;
+        }
+    };
+    auto store_block = [&](int slot, const uint32_t *src) {
+        for (int g = lane; g < kMtN / 4; g += kWave) {
+            u32x4 x = *reinterpret_cast<const u32x4 *>(src + 4 * g);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = mt_temper(x[i]);
+            *reinterpret_cast<u32x4 *>(blk + slot * kMtN + 4 * g) = x;
+        }
+    };
+    load_block(cur, A);
     wave_lds_fence();
     if (mti >= kMtN) {
         mt_twist_wave(A, B, lane);
@@ -2167,10 +2183,10 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
         B = x;
         cur ^= 1;
         mti -= kMtN;
-        for (int k = lane; k < kMtN; k += kWave) blk[cur * kMtN + k] = A[k];
+        store_block(cur, A);
     }
     mt_twist_wave(A, B, lane);
-    for (int k = lane; k < kMtN; k += kWave) blk[(cur ^ 1) * kMtN + k] = B[k];
+    store_block(cur ^ 1, B);
     if (lane == 0) rs.pos[e] = (cur << 16) | kMtNextReady | mti;
 }
 
@@ -2254,7 +2270,8 @@ struct MtRingT {
 #pragma unroll
             for (int g = 0; g < kRing / 8; ++g)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) ring[((tail + 4 * g + i) & (kRing - 1)) * ENVS] = mt_temper(x[g][i]);
+                for (int i = 0; i < 4; ++i)
+                    ring[((tail + 4 * g + i) & (kRing - 1)) * ENVS] = x[g][i];   // tempered in HBM
             tail += kRing / 2;
         }
     }
@@ -2271,7 +2288,7 @@ struct MtRingT {
             const int g = head & ~3;
             const u32x4 x = *reinterpret_cast<const u32x4 *>(word_ptr(g));
 #pragma unroll
-            for (int i = 0; i < 4; ++i) ring[((g + i) & (kRing - 1)) * ENVS] = mt_temper(x[i]);
+            for (int i = 0; i < 4; ++i) ring[((g + i) & (kRing - 1)) * ENVS] = x[i];
             tail = g + 4;
         }
         const uint32_t y = ring[(head & (kRing - 1)) * ENVS];
@@ -2729,7 +2746,7 @@ __global__ __launch_bounds__(256) void py_ratio_kernel(RefStreams ps, double *__
             mti -= kMtN;
             ready = false;
         }
-        return mt_temper(blk[cur * kMtN + mti++]);
+        return blk[cur * kMtN + mti++];   // tempered in HBM
     };
     auto randint180 = [&]() -> int {   // random.randint(0, 180): _randbelow(181), getrandbits(8) rejection
         uint32_t r;

@@ -121,13 +121,33 @@ struct Params {
 // env, env-major ([E][2][624] u32: one env's words are contiguous, so a lane drawing from its own
 // stream reads consecutive words).  pos[e] = cur << 16 | mti: block `cur` holds the state whose
 // tempered words mti..623 are the stream's next draws; mt_prepare_kernel puts the state one twist
-// later into the other block before a day is drawn.  The Python `random` stream (two or three draws a
-// day) stays on the host (sng_mt.h).
+// later into the other block before a day is drawn.  Python's `random` stream of every env (two or
+// three draws a day) is kept the same way (py_ratio_kernel draws it).
+// The blocks hold the state words TEMPERED (the stream's output words): the drawing kernels read their
+// words as they are, and the twisting kernels untemper what they read and temper what they write
+// (mt_temper_word / mt_untemper_word, a bijection).  Checkpoints export numpy's raw state.
 struct RefStreams {
     uint32_t *mt;
     int32_t *pos;
 };
 constexpr int kMtN = 624, kMtM = 397;
+SNG_HD inline uint32_t mt_temper_word(uint32_t y) {
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+SNG_HD inline uint32_t mt_untemper_word(uint32_t y) {
+    y ^= y >> 18;                   // shifts of >= 16 bits undo in one step
+    y ^= (y << 15) & 0xefc60000u;
+    uint32_t t = y;                 // << 7: 5 steps cover 32 bits
+#pragma unroll
+    for (int i = 0; i < 4; ++i) t = y ^ ((t << 7) & 0x9d2c5680u);
+    y = t;
+    t = y ^ (y >> 11);              // >> 11: 3 steps
+    return y ^ (t >> 11);
+}
 // RefStreams::pos word: cur << 16 | kMtNextReady | mti (mti <= 624)
 constexpr int32_t kMtNextReady = 0x4000, kMtPosMask = 0x3fff;
 

@@ -106,3 +106,32 @@ def test_state_refuses_inconsistent_headers():
     assert torch.equal(a.replay_tensors(), b.replay_tensors())
     a.close()
     b.close()
+
+
+def test_exported_streams_are_numpy_and_python_states():
+    """The blob's stream section is numpy's RandomState state and Python's random state of every env (raw
+    MT19937 words and position; the device keeps its blocks tempered, sng_layout.h RefStreams): after one
+    reference-RNG reset, Python's stream is random.Random(seed + i) after the day's randint(0, 180)
+    (smart_nanogrid_environment.py:349) and numpy's is RandomState(seed + i) some words further on."""
+    import random
+    E, seed = 32, 11
+    kw = dict(number_of_chargers=4, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+    a = SmartNanogridVecEnv(E, seed=seed, rng="reference", **kw)
+    a.reset_tensors()
+    blob = a.save_state()
+    a.close()
+    w = np.frombuffer(blob, dtype=np.uint32, count=E * 2 * 625, offset=len(blob) - E * 2 * 625 * 4).reshape(E, 2, 625)
+    for i in range(E):
+        r = random.Random(seed + i)
+        r.randint(0, 180)
+        st = r.getstate()[1]
+        assert list(w[i, 1, :624]) == list(st[:624]) and int(w[i, 1, 624]) == st[624], i
+        rs = np.random.RandomState(seed + i)
+        for k in range(4000):   # the day drew k words: one 32-bit word per uint32 randint of full range
+            _, key, pos = rs.get_state()[:3]
+            if pos == int(w[i, 0, 624]) and np.array_equal(key, w[i, 0, :624]):
+                break
+            rs.randint(0, 2**32, dtype=np.uint32)
+        else:
+            raise AssertionError(f"env {i}: the exported numpy state is not RandomState({seed + i}) after any draw count")
+        assert k > 0
