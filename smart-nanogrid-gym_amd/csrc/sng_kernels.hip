@@ -1566,35 +1566,63 @@ constexpr int kGenBlock = 256;       // 4 waves of consecutive envs, same charge
 constexpr int kDayVehicles = 8;
 constexpr float kInvLog2Q = -1.3569154488567239f;   // 1 / log2(0.6)
 
+// LDS slots per thread: the list's kDayVehicles entries and one more, which phase 2's look-ahead may
+// read (never use) once the walk has reached the sentinel in slot 7
+constexpr int kDaySlots = kDayVehicles + 1;
 __host__ __device__ constexpr size_t generate_lds_bytes(bool with_req) {
-    return (size_t)kDayVehicles * kGenBlock * (sizeof(uint32_t) + sizeof(float) + (with_req ? sizeof(double) : 0));
+    return (size_t)kDaySlots * kGenBlock * (sizeof(uint32_t) + sizeof(float) + (with_req ? sizeof(double) : 0));
 }
 
 // One vehicle's draws (charging_station.py:257-279), in stream order: the geometric wait from
 // tfree to the arrival, arrival SoC, capacity + departure, requested SoC.  Phase 1 below and the
 // t = 0 observation blocks share it, so both see the same first vehicle.
+// Two 32-bit draws per vehicle (three with requested SoC), from a two-multiply hash (GenStream):
+// the generator is bound by the VALU it issues (18.4 us for ~1,000 VALU per (env, charger) thread
+// at 65,536 x 10), and the draws were a third of it.  x1's top 24 bits give the geometric wait, x2's
+// top 24 bits the SoC (a float32 value in [0.1f, 0.9f], computed in float), and the 16 low bits of
+// the two drive capacity (floor(r * 105 / 2^16)) and, through the low half of r * 105 (a bijection
+// of r, as 105 is odd), the departure.
 struct VehicleDraw {
     int ta, dep;
     uint32_t cap;
     double soc;
     uint32_t req_draw;
 };
-__device__ __forceinline__ VehicleDraw draw_vehicle(const Params &p, HashStream &rng, int tfree, int i4, int i10,
+__device__ __forceinline__ uint32_t mix32_gen(uint32_t x) {   // "lowbias32" (two multiplies, bijective)
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+struct GenStream {
+    uint32_t key, ctr;
+    __device__ __forceinline__ uint32_t next() { return mix32_gen(key + (ctr++) * 0x9e3779b9u); }
+};
+// Stream key of (seed, global env, charger, day) for the generator: one hash per (env, charger) over the
+// index ge * 128 + c (unique for ge < 2^25 and c < 128, the ABI's maximum station), the day's seed hash k0
+// offset by ge >> 25 beyond that.  k0 is wave-uniform (scalar).
+__device__ __forceinline__ uint32_t gen_key(uint64_t seed, uint64_t ge, uint32_t c, uint64_t day) {
+    const uint32_t k0 = mix32((uint32_t)seed ^ mix32((uint32_t)(seed >> 32) + (uint32_t)day * 0x9e3779b9u));
+    return mix32((k0 + (uint32_t)(ge >> 25) * 0x85ebca6bu) ^ (((uint32_t)ge << 7) | c));
+}
+__device__ __forceinline__ VehicleDraw draw_vehicle(const Params &p, GenStream &rng, int tfree, int i4, int i10,
                                                     int i1) {
     VehicleDraw d;
-    const float u = ((float)(rng.next() >> 8) + 1.0f) * 0x1.0p-24f;   // (0, 1]
-    d.ta = tfree + (int)(__log2f(u) * kInvLog2Q);                       // floor: the product is >= 0
-    // uniform(0.1, 0.9), drawn as a float32 value (the packed record holds it exactly)
-    d.soc = (double)(float)(0.1 + (0.9 - 0.1) * u32_unit(rng.next()));
-    // capacity and departure from one draw: cap = floor(y * 105 / 2^32); the low word of
-    // y * 105 (a bijection of y, uniform given cap) drives the departure
-    const uint32_t y = rng.next();
-    d.cap = p.diff_caps ? (uint32_t)(15 + below(y, 105)) : 40u;   // randint(15, 120)
-    const uint32_t yd = p.diff_caps ? y * 105u : y;
+    const uint32_t x1 = rng.next(), x2 = rng.next();
+    const float u = ((float)(x1 >> 8) + 1.0f) * 0x1.0p-24f;   // (0, 1]
+    d.ta = tfree + (int)(__log2f(u) * kInvLog2Q);               // floor: the product is >= 0
+    // uniform(0.1, 0.9) as a float32 value (the packed record holds it exactly): at most 0.9f
+    d.soc = (double)(0.1f + 0.8f * ((float)(x2 >> 8) * 0x1.0p-24f));
+    const uint32_t r = ((x1 & 0xffu) << 8) | (x2 & 0xffu);
+    const uint32_t rc = r * 105u;
+    d.cap = p.diff_caps ? 15u + (rc >> 16) : 40u;   // randint(15, 120)
+    const uint32_t yd = (p.diff_caps ? rc : r) & 0xffffu;
     const int hi_c = d.ta + i10, hi_d = p.T + i1;
     const int high = hi_c < hi_d ? hi_c : hi_d;
     const int low = d.ta + i4;
-    d.dep = (low >= high) ? low : low + below(yd, high - low);
+    d.dep = (low >= high) ? low : low + (int)(__umul24(yd, (uint32_t)(high - low)) >> 16);   // 16 x 8 bits
     d.req_draw = p.req_enabled ? rng.next() : 0u;
     return d;
 }
@@ -1639,7 +1667,7 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
         const int k = p.pv ? 8 : 4;
         const uint32_t el8 = (uint32_t)e * 8u;
         for (int c = 0; c < n; ++c) {
-            HashStream rng{stream_key(seed, ge, (uint32_t)c, day), 0u};
+            GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
             const VehicleDraw d = draw_vehicle(p, rng, 0, i4, i10, i1);
             const bool occ0 = d.ta == 0;   // t = 0 < T always, and dep >= 4/dt > 0
             const double soc0 = occ0 ? d.soc : 0.0;
@@ -1681,8 +1709,8 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
                                                              double *__restrict__ ep_return, int vec_io) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     uint32_t *s_veh = reinterpret_cast<uint32_t *>(lds);                      // [V][BLOCK] arr | cap<<8 | dep<<16
-    uint32_t *s_car = s_veh + kDayVehicles * kGenBlock;                        // [V][BLOCK] arrival SoC carry bits
-    double *s_req = reinterpret_cast<double *>(s_car + kDayVehicles * kGenBlock);   // [V][BLOCK] (REQ only)
+    uint32_t *s_car = s_veh + kDaySlots * kGenBlock;                           // [V][BLOCK] arrival SoC carry bits
+    double *s_req = reinterpret_cast<double *>(s_car + kDaySlots * kGenBlock);     // [V][BLOCK] (REQ only)
     const int tid = threadIdx.x;
     const int64_t e = (int64_t)blockIdx.x * kGenBlock + tid;
     const int c = blockIdx.y;
@@ -1695,7 +1723,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     }
     if (e >= E) return;
     const uint64_t ge = (uint64_t)(e + p.env_offset);   // global env id
-    HashStream rng{stream_key(seed, ge, (uint32_t)c, day), 0u};
+    GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
     const int T = TT > 0 ? TT : p.T;
     const int n = p.n;
 
@@ -1732,9 +1760,12 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     uint32_t cur = s_veh[tid], nxt = s_veh[kGenBlock + tid];
     uint32_t car_cur = s_car[tid], car_nxt = s_car[kGenBlock + tid];
     double req_cur = REQ ? s_req[tid] : 1.0, req_nxt = REQ ? s_req[kGenBlock + tid] : 1.0;
-    int v = 0;
+    int nx = kGenBlock + tid;   // the slot of list[v + 1]
     bool prev_occ = false;
-    uint32_t prev_rem = 0u;
+    bool pen = false;   // step t is in the penalty-check list observe(t-1) built
+    // step t occupied / its vehicle arriving at t, carried from step to step: step t + 1 is occupied iff
+    // its vehicle arrives then (arr1) or step t's vehicle stays past t + 1
+    bool occ = (cur & 0xffu) == 0u, stat = occ;
     // penalty-check list built by observe(t-1) (charging_station.py:42-63) as one unsigned range
     // test on the steps the vehicle at t-1 had left: on_departure {1}, sparse {1..3}, dense any;
     // no_penalty never (lo = 256 > any remainder)
@@ -1755,18 +1786,15 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const uint32_t v1 = adv ? nxt : cur;
         const uint32_t car1 = adv ? car_nxt : car_cur;
         const double req1 = adv ? req_nxt : req_cur;
-        v += adv ? 1 : 0;
-        const int vr = v + 1 < kDayVehicles ? v + 1 : kDayVehicles - 1;   // list[v + 1] for step t + 1
-        const uint32_t nxt1 = s_veh[vr * kGenBlock + tid];
-        const uint32_t car_nxt1 = s_car[vr * kGenBlock + tid];
-        const double req_nxt1 = REQ ? s_req[vr * kGenBlock + tid] : 1.0;
+        nx += adv ? kGenBlock : 0;   // list[v + 1] for step t + 1 (slot 8 at most, kDaySlots)
+        const uint32_t nxt1 = s_veh[nx];
+        const uint32_t car_nxt1 = s_car[nx];
+        const double req_nxt1 = REQ ? s_req[nx] : 1.0;
 
-        const uint32_t ta = cur & 0xffu, dep = cur >> W_DEP_SHIFT;
-        const bool occ = (uint32_t)t >= ta && (uint32_t)t < dep;
-        const bool pen = prev_rem - pen_lo <= pen_span;   // prev_rem = 0: charger empty at t-1
-        const uint32_t flags = W_OCC | ((uint32_t)t == ta ? W_STATIC : 0u) | (pen ? W_PEN : 0u);
+        const uint32_t flags = W_OCC | (stat ? W_STATIC : 0u) | (pen ? W_PEN : 0u);
         const uint32_t w_occ = ((cur & 0xffff00u) | flags) - ((uint32_t)t << W_DEP_SHIFT);   // dep -> dep - t
-        const uint32_t carry = ((v1 & 0xffu) == (uint32_t)(t + 1)) ? car1 : 0u;
+        const bool arr1 = (v1 & 0xffu) == (uint32_t)(t + 1);   // step t + 1's vehicle arrives then
+        const uint32_t carry = arr1 ? car1 : 0u;
         const uint32_t w_emp = (pen ? W_PEN : 0u) | carry;
 #ifdef SNG_GX_NOPH2
         if ((occ ? w_occ : w_emp) == 0xdeadbeefu)
@@ -1776,7 +1804,11 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
         if (REQ && t > 0) bst(s.req + (size_t)t * nE, el8, prev_occ ? req_cur : 0.0, r8);
         prev_occ = occ;
-        prev_rem = occ ? dep - (uint32_t)t : 0u;
+        // step t + 1's penalty check: occupied at t with dep - t steps left in [pen_lo, pen_lo + pen_span]
+        // (w_occ's departure field holds dep - t; an empty charger is never in the list)
+        pen = occ && (w_occ >> W_DEP_SHIFT) - pen_lo <= pen_span;
+        occ = (occ && (uint32_t)(t + 1) < (cur >> W_DEP_SHIFT)) || arr1;
+        stat = arr1;
         cur = v1;
         car_cur = car1;
         req_cur = req1;
