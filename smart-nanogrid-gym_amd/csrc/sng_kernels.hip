@@ -1632,41 +1632,54 @@ __device__ __forceinline__ VehicleDraw draw_vehicle(const Params &p, GenStream &
 // timeline blocks (SmartNanogridEnv.reset -> __get_observations, smart_nanogrid_environment.py:
 // 349-351): each charger's first vehicle, if it arrives at t = 0, gives SOC[c, 0] and the
 // departure entry; the PV ratio, the day's profile factors, the header and the BESS entry; the
-// running SoC is seeded and the day return zeroed.  Thread = env; rows leave through LDS.
+// running SoC is seeded and the day return zeroed.  Four threads per env (chargers and profile
+// entries dealt round-robin, the header on the first), 64 envs per block: grid rows y = N .. N + 3
+// cover a timeline block's 256 envs.  A thread's work is then a few vehicles, like a timeline
+// thread's, instead of the whole station (one thread per env ran ~10x longer and finished last), and
+// the 64-row tile (7.4 KB at N = 10) no longer caps the grid at 5 workgroups per CU.
+constexpr int kObsParts = 4;                       // threads per env
+constexpr int kObsEnvs = kGenBlock / kObsParts;    // envs per observation block
+constexpr int kObsBlocks = kGenBlock / kObsEnvs;   // observation blocks per 256 envs
 __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4,
                                              int i10, int i1, uint64_t day, float *__restrict__ obs,
-                                             double *__restrict__ ep_return, int vec_io, float *lds) {
+                                             double *__restrict__ ep_return, int vec_io, float *lds, int q) {
     const int n = p.n, O = p.obs_dim;
-    const int tid = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * kGenBlock;
-    const int nblk = (int)((E - e0) < kGenBlock ? (E - e0) : kGenBlock);
-    const int64_t e = e0 + tid;
-    float *o_row = lds + tid * O;
-    if (tid < nblk) {
+    const int tid = threadIdx.x, part = tid % kObsParts, le = tid / kObsParts;
+    const int64_t e0 = (int64_t)blockIdx.x * kGenBlock + (int64_t)q * kObsEnvs;
+    if (e0 >= E) return;   // the whole block (before any barrier)
+    const int nblk = (int)((E - e0) < kObsEnvs ? (E - e0) : kObsEnvs);
+    const int64_t e = e0 + le;
+    float *o_row = lds + le * O;
+    if (le < nblk) {
         const uint64_t ge = (uint64_t)(e + p.env_offset);
-        const double ratio = pv_ratio_draw(seed, ge, day);
-        s.ratio[e] = ratio;
-        s.pen0[e] = 0.0;
-        double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
-        if (p.noise) {   // the day's profile factors prof[2][T + 3][E] (profile_kernel's)
-            const uint64_t env_seed = p.seed + (uint64_t)p.env_offset + (uint64_t)e;
+        const uint64_t env_seed = p.seed + (uint64_t)p.env_offset + (uint64_t)e;
+        if (p.noise) {   // the day's profile factors prof[2][T + 3][E] (profile_kernel's), k = part mod 4
             const size_t pl = (size_t)(p.T + 3) * E;
-            for (int k = 0; k < p.T + 3; ++k) {
-                const double a = p.pv_noise != 0.0 ? profile_factor(env_seed, kDomainPV, day, k, p.pv_noise) : 1.0;
-                const double b =
+            for (int k = part; k < p.T + 3; k += kObsParts) {
+                s.prof[(size_t)k * E + e] = p.pv_noise != 0.0 ? profile_factor(env_seed, kDomainPV, day, k, p.pv_noise) : 1.0;
+                s.prof[pl + (size_t)k * E + e] =
                     p.price_noise != 0.0 ? profile_factor(env_seed, kDomainPrice, day, k, p.price_noise) : 1.0;
-                s.prof[(size_t)k * E + e] = a;
-                s.prof[pl + (size_t)k * E + e] = b;
-                if (k < 4) {
-                    fpv[k] = a;
-                    fpr[k] = b;
-                }
             }
         }
-        write_obs_header(o_row, p, s.tables->irr_norm, s.tables->price_norm, ratio, fpv, fpr);
+        if (part == 0) {
+            const double ratio = pv_ratio_draw(seed, ge, day);
+            s.ratio[e] = ratio;
+            s.pen0[e] = 0.0;
+            double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
+            if (p.noise) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (p.pv_noise != 0.0) fpv[k] = profile_factor(env_seed, kDomainPV, day, k, p.pv_noise);
+                    if (p.price_noise != 0.0) fpr[k] = profile_factor(env_seed, kDomainPrice, day, k, p.price_noise);
+                }
+            }
+            write_obs_header(o_row, p, s.tables->irr_norm, s.tables->price_norm, ratio, fpv, fpr);
+            if (p.bess) o_row[O - 1] = (float)s.bess[e];
+            if (ep_return) ep_return[e] = 0.0;
+        }
         const int k = p.pv ? 8 : 4;
         const uint32_t el8 = (uint32_t)e * 8u;
-        for (int c = 0; c < n; ++c) {
+        for (int c = part; c < n; c += kObsParts) {
             GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
             const VehicleDraw d = draw_vehicle(p, rng, 0, i4, i10, i1);
             const bool occ0 = d.ta == 0;   // t = 0 < T always, and dep >= 4/dt > 0
@@ -1675,8 +1688,6 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
             o_row[k + c] = (float)soc0;
             o_row[k + n + c] = departure_obs(pack_word(occ0, occ0, false, 0u, occ0 ? (uint32_t)d.dep : 0u));
         }
-        if (p.bess) o_row[O - 1] = (float)s.bess[e];
-        if (ep_return) ep_return[e] = 0.0;
     }
     __syncthreads();
     copy_out<kGenBlock>(obs + e0 * O, lds, nblk * O, vec_io != 0, tid);
@@ -1688,7 +1699,7 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 //     then arrival SoC, capacity and departure -- a few draws per vehicle instead of one per free
 //     step, without the per-step divergent arrival branch;
 //  2. the dense timeline, step by step, from the vehicle list kept in LDS.
-// Grid (E / 256, N + 1): blocks y < N write charger y's timeline, blocks y = N the t = 0
+// Grid (E / 256, N + 4): blocks y < N write charger y's timeline, blocks y >= N the t = 0
 // observation (observe_day0).  The day counter is read here and advanced by the day's first step
 // (step_kernel, t = 0), so no block of this grid waits on another.
 // The timeline records leave as streaming (nontemporal) stores: reset 24.5-24.7 -> 22.5-22.7 us per day
@@ -1715,9 +1726,9 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     const int64_t e = (int64_t)blockIdx.x * kGenBlock + tid;
     const int c = blockIdx.y;
     const uint64_t day = *s.episode;
-    if (c == p.n) {
+    if (c >= p.n) {
 #ifndef SNG_GX_NOOBS   // diagnostic builds (tools/gpu_session.sh ablib) only: generator cost breakdown
-        observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds);
+        observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds, c - p.n);
 #endif
         return;
     }
@@ -2085,10 +2096,15 @@ hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hip
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            float *obs, double *ep_return, int vec_io, hipStream_t stream, hipEvent_t ev_start,
                            hipEvent_t ev_stop) {
-    const size_t veh = generate_lds_bytes(p.req_enabled != 0), tile = (size_t)round4(kGenBlock * p.obs_dim) * 4;
-    const bool fused = tile <= 48 * 1024;
-    const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(p.n + (fused ? 1 : 0))), block(kGenBlock);
+    const size_t veh = generate_lds_bytes(p.req_enabled != 0), tile = (size_t)round4(kObsEnvs * p.obs_dim) * 4;
+    const bool fused = tile <= 32 * 1024;   // up to 60 chargers (config 5's 50: 27.9 KB)
+    const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(p.n + (fused ? kObsBlocks : 0))),
+        block(kGenBlock);
+#ifdef SNG_GX_SMALL_LDS   // diagnostic builds only (with SNG_GX_NOOBS): the list's LDS alone
+    const size_t lds = veh;
+#else
     const size_t lds = (fused && tile > veh) ? tile : veh;
+#endif
     const bool req = p.req_enabled != 0;
     auto kern = p.T == 24 ? (req ? generate_kernel<24, true> : generate_kernel<24, false>)
                           : (req ? generate_kernel<0, true> : generate_kernel<0, false>);
