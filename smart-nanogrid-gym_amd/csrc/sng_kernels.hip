@@ -1632,19 +1632,21 @@ __device__ __forceinline__ VehicleDraw draw_vehicle(const Params &p, GenStream &
 // timeline blocks (SmartNanogridEnv.reset -> __get_observations, smart_nanogrid_environment.py:
 // 349-351): each charger's first vehicle, if it arrives at t = 0, gives SOC[c, 0] and the
 // departure entry; the PV ratio, the day's profile factors, the header and the BESS entry; the
-// running SoC is seeded and the day return zeroed.  Four threads per env (chargers and profile
-// entries dealt round-robin, the header on the first), 64 envs per block: grid rows y = N .. N + 3
+// running SoC is seeded and the day return zeroed.  64 envs per block, lane = env, and the block's
+// four wavefronts split the row: wavefront 0 the header (PV ratio, profile factors, BESS entry),
+// wavefronts 1-3 the chargers round-robin; profile entries go to all four.  Grid rows y = N .. N + 3
 // cover a timeline block's 256 envs.  A thread's work is then a few vehicles, like a timeline
-// thread's, instead of the whole station (one thread per env ran ~10x longer and finished last), and
-// the 64-row tile (7.4 KB at N = 10) no longer caps the grid at 5 workgroups per CU.
-constexpr int kObsParts = 4;                       // threads per env
+// thread's, instead of the whole station (one thread per env ran ~10x longer and finished last),
+// no wavefront runs the header under a mask, and the 64-row tile (7.4 KB at N = 10) no longer caps
+// the grid at 5 workgroups per CU.
+constexpr int kObsParts = kGenBlock / kWave;       // wavefronts per observation block (threads per env)
 constexpr int kObsEnvs = kGenBlock / kObsParts;    // envs per observation block
 constexpr int kObsBlocks = kGenBlock / kObsEnvs;   // observation blocks per 256 envs
 __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4,
                                              int i10, int i1, uint64_t day, float *__restrict__ obs,
                                              double *__restrict__ ep_return, int vec_io, float *lds, int q) {
     const int n = p.n, O = p.obs_dim;
-    const int tid = threadIdx.x, part = tid % kObsParts, le = tid / kObsParts;
+    const int tid = threadIdx.x, part = __builtin_amdgcn_readfirstlane(tid / kWave), le = tid % kWave;
     const int64_t e0 = (int64_t)blockIdx.x * kGenBlock + (int64_t)q * kObsEnvs;
     if (e0 >= E) return;   // the whole block (before any barrier)
     const int nblk = (int)((E - e0) < kObsEnvs ? (E - e0) : kObsEnvs);
@@ -1679,7 +1681,7 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
         }
         const int k = p.pv ? 8 : 4;
         const uint32_t el8 = (uint32_t)e * 8u;
-        for (int c = part; c < n; c += kObsParts) {
+        for (int c = part - 1; part > 0 && c < n; c += kObsParts - 1) {
             GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
             const VehicleDraw d = draw_vehicle(p, rng, 0, i4, i10, i1);
             const bool occ0 = d.ta == 0;   // t = 0 < T always, and dep >= 4/dt > 0
@@ -1699,8 +1701,8 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 //     then arrival SoC, capacity and departure -- a few draws per vehicle instead of one per free
 //     step, without the per-step divergent arrival branch;
 //  2. the dense timeline, step by step, from the vehicle list kept in LDS.
-// Grid (E / 256, N + 4): blocks y < N write charger y's timeline, blocks y >= N the t = 0
-// observation (observe_day0).  The day counter is read here and advanced by the day's first step
+// Grid (E / 256, 4 + N): blocks y < 4 the t = 0 observation (observe_day0), blocks y >= 4 charger
+// y - 4's timeline.  The day counter is read here and advanced by the day's first step
 // (step_kernel, t = 0), so no block of this grid waits on another.
 // The timeline records leave as streaming (nontemporal) stores: reset 24.5-24.7 -> 22.5-22.7 us per day
 // at 65,536 x 10 (A/B, one box), the steps' code and state staying in L2.  Diagnostic builds
@@ -1724,11 +1726,14 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     double *s_req = reinterpret_cast<double *>(s_car + kDaySlots * kGenBlock);     // [V][BLOCK] (REQ only)
     const int tid = threadIdx.x;
     const int64_t e = (int64_t)blockIdx.x * kGenBlock + tid;
-    const int c = blockIdx.y;
+    // grid rows: the t = 0 observation blocks first (gridDim.y - N of them: dispatched first, their
+    // dependent table and BESS loads do not trail the timeline blocks), then charger c = y - rows
+    const int obs_rows = (int)gridDim.y - p.n;
+    const int c = (int)blockIdx.y - obs_rows;
     const uint64_t day = *s.episode;
-    if (c >= p.n) {
+    if (c < 0) {
 #ifndef SNG_GX_NOOBS   // diagnostic builds (tools/gpu_session.sh ablib) only: generator cost breakdown
-        observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds, c - p.n);
+        observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds, (int)blockIdx.y);
 #endif
         return;
     }
