@@ -2102,7 +2102,10 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
                            float *obs, double *ep_return, int vec_io, hipStream_t stream, hipEvent_t ev_start,
                            hipEvent_t ev_stop) {
     const size_t veh = generate_lds_bytes(p.req_enabled != 0), tile = (size_t)round4(kObsEnvs * p.obs_dim) * 4;
-    const bool fused = tile <= 32 * 1024;   // up to 60 chargers (config 5's 50: 27.9 KB)
+#ifndef SNG_GX_FUSE_MAX
+#define SNG_GX_FUSE_MAX (32 * 1024)
+#endif
+    const bool fused = tile <= SNG_GX_FUSE_MAX;   // up to 60 chargers (config 5's 50: 27.9 KB)
     const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(p.n + (fused ? kObsBlocks : 0))),
         block(kGenBlock);
 #ifdef SNG_GX_SMALL_LDS   // diagnostic builds only (with SNG_GX_NOOBS): the list's LDS alone
@@ -2111,8 +2114,12 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
     const size_t lds = (fused && tile > veh) ? tile : veh;
 #endif
     const bool req = p.req_enabled != 0;
+#ifndef SNG_GX_T96
+#define SNG_GX_T96 1
+#endif
     auto kern = p.T == 24 ? (req ? generate_kernel<24, true> : generate_kernel<24, false>)
-                          : (req ? generate_kernel<0, true> : generate_kernel<0, false>);
+                : (SNG_GX_T96 && p.T == 96 && !req) ? generate_kernel<96, false>   // config 5's 15-minute day
+                : (req ? generate_kernel<0, true> : generate_kernel<0, false>);
     if (fused && ev_start && ev_stop) {   // the one-launch reset, timed by its own dispatch timestamps
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev_start, ev_stop, 0u, p, s, seed, E, i4, i10, i1, obs,
                               ep_return, vec_io);
