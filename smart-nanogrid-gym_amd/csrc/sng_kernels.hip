@@ -1862,6 +1862,33 @@ hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, 
 }
 
 // ---------------------------------------------------------------------------------
+// The reference's rule-based controller (solvers/RBC/rbc.py:6-29), one thread per action entry
+// (coalesced action stores; an env's departure entries are adjacent).  Comparisons and the average in
+// float32, as numpy does on the float32 observation with a Python-float threshold (NEP 50).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void rbc_kernel(const float *__restrict__ obs, float *__restrict__ act,
+                                                  uint32_t total, uint32_t N, uint32_t A, uint32_t O) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= total) return;
+    const uint32_t e = i / A, j = i - e * A;
+    float a = 0.f;   // the BESS entry, and an empty charger
+    if (j < N) {
+        const float *o = obs + (size_t)e * O;
+        const float d = o[8u + N + j];
+        a = (d == 0.f) ? 0.f : (d > 0.f && d < 0.16667f) ? 1.f : (o[0] + o[2]) / 2.f;
+    }
+    act[i] = a;
+}
+
+hipError_t launch_rbc(const float *obs, float *act, int64_t E, int N, int bess, hipStream_t stream) {
+    const uint32_t A = (uint32_t)(N + (bess ? 1 : 0)), O = (uint32_t)(2 * N + 8 + (bess ? 1 : 0));
+    const uint32_t total = (uint32_t)E * A;
+    hipLaunchKernelGGL(rbc_kernel, dim3((total + 255u) / 256u), dim3(256), 0, stream, obs, act, total, (uint32_t)N, A,
+                       O);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
 // launch wrappers (called from sng_api.cpp)
 // ---------------------------------------------------------------------------------
 // Optional start/stop events: hipExtLaunchKernel stamps them with the dispatch's own

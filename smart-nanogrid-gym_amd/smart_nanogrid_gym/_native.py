@@ -142,6 +142,8 @@ EXPORTS = {
     "sng_get_day_counter": (ctypes.c_int, [_H, ctypes.POINTER(ctypes.c_uint64), _S]),
     "sng_bandwidth_probe": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), _S]),
+    "sng_rule_based_actions": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                              ctypes.c_int32, _S]),
     "sng_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "sng_comm_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                        ctypes.POINTER(ctypes.c_void_p)]),
