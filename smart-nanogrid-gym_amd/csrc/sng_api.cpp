@@ -31,7 +31,8 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
                        double *reward, uint8_t *done, int64_t E, int t, int vec_io, hipStream_t stream,
                        hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
-                           int vec_io, hipStream_t stream, int mode, int64_t replay);
+                           int vec_io, hipStream_t stream, int mode, int64_t replay, const RefStreams *ps = nullptr,
+                           int py = 0);
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            float *obs, double *ep_return, int vec_io,
                            hipStream_t stream, hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr);
@@ -42,7 +43,6 @@ hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, 
 hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream);
 hipError_t launch_mt_prepare(const RefStreams &rs, int64_t E, hipStream_t stream);
 hipError_t launch_rbc(const float *obs, float *act, int64_t E, int N, int bess, hipStream_t stream);
-hipError_t launch_py_ratio(const RefStreams &ps, double *ratio, int64_t E, int end_draw, int draw, hipStream_t stream);
 hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
                           int i1, bool prepare, hipStream_t stream);
 int step_lanes_supported(int n, int lanes);
@@ -514,7 +514,7 @@ struct SngEnv {
     bool prep_launched = false;   // prep_done marks a prepare launched on prep_stream
 
     bool prepared = false;        // the next day's blocks are (being) prepared: no inline prepare
-    RefStreams ps{};                  // Python's `random` stream of every env, on the device (py_ratio_kernel)
+    RefStreams ps{};                  // Python's `random` stream of every env, on the device (py_ratio_lane in observe0_kernel)
     bool py_seeded = false;
     std::string err;
 
@@ -613,7 +613,7 @@ int ensure_staging(SngEnv *env, bool with_req) {
 // The reference's global RNG streams of every env, np.random.seed(s) and random.seed(s) with
 // s = seed + global env index (SngRngMode SNG_RNG_REFERENCE), both on the device.  Python's is seeded on
 // the host threads (CPython's init_by_array, sng_mt.h) and uploaded once into the RefStreams layout
-// (block 0, position N: the first draw twists), then drawn by py_ratio_kernel: random.randint(0, 180)
+// (block 0, position N: the first draw twists), then drawn by observe0_kernel (py_ratio_lane): random.randint(0, 180)
 // for a reset's PV ratio, after the day-end draw the last step owes (smart_nanogrid_environment.py:181, 349).
 int await_prepare(SngEnv *env, hipStream_t st);
 int ensure_py_streams(SngEnv *env, hipStream_t st) {
@@ -641,7 +641,7 @@ int ensure_py_streams(SngEnv *env, hipStream_t st) {
     HIP_TRY(env, hipMemcpy2DAsync(env->ps.mt, 2 * kMtN * sizeof(uint32_t), words.data(), kMtN * sizeof(uint32_t),
                                   kMtN * sizeof(uint32_t), E, hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipMemcpyAsync(env->ps.pos, pos.data(), E * sizeof(int32_t), hipMemcpyHostToDevice, st));
-    // the first twist by a wavefront per env now, not by py_ratio_kernel's one lane at the first draw
+    // the first twist by a wavefront per env now, not by py_ratio_lane at the first draw
     HIP_TRY(env, launch_mt_prepare(env->ps, env->E, st));
     HIP_TRY(env, hipStreamSynchronize(st));   // the host vectors go out of scope
     env->py_seeded = true;
@@ -778,14 +778,13 @@ int build_and_upload(SngEnv *env, int req_upload, hipStream_t st, bool *need_req
 }
 
 // After the day's planes: the PV ratios and t = 0 penalties, then the t = 0 observation.  py_end / py_draw:
-// the Python streams' owed day-end draw / the ratio drawn on the device (py_ratio_kernel) over the upload.
+// the Python streams' owed day-end draw / the ratio drawn on the device (in observe0_kernel) over the upload.
 int finish_host_day(SngEnv *env, bool req_stream, float *obs, hipStream_t st, int py_end, int py_draw) {
     HIP_TRY(env, hipMemcpyAsync(env->ds.ratio, env->h_ratio, env->E * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipMemcpyAsync(env->ds.pen0, env->h_pen0, env->E * sizeof(double), hipMemcpyHostToDevice, st));
-    if (py_end || py_draw) {
+    if (py_end || py_draw) {   // the draws themselves run inside observe0_kernel below
         int rc = await_prepare(env, st);
         if (rc) return rc;
-        HIP_TRY(env, launch_py_ratio(env->ps, env->ds.ratio, env->E, py_end, py_draw, st));
     }
     HIP_TRY(env, hipEventRecord(env->staging_done, st));
     env->p.req_stream = req_stream ? 1 : 0;
@@ -793,7 +792,8 @@ int finish_host_day(SngEnv *env, bool req_stream, float *obs, hipStream_t st, in
     env->p.req_zero = 0;
     env->p.bump_day = 0;
     HIP_TRY(env, sng::launch_profiles(env->p, env->ds, env->E, st));
-    HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st, OBS0_HOST, -1));
+    HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st, OBS0_HOST, -1,
+                                      &env->ps, (py_draw ? 1 : 0) | (py_end ? 2 : 0)));
     env->t = 0;
     env->day_finished = false;
     return SNG_OK;
@@ -1131,14 +1131,14 @@ int sng_reset(SngEnv *env, int rng_mode, float *obs, void *stream) {
     }
     env->p.req_stream = with_req ? 1 : 0;
     HIP_TRY(env, launch_ref_day(env->p, env->ds, env->rs, env->E, env->i4, env->i10, env->i1, !env->prepared, st));
-    HIP_TRY(env, launch_py_ratio(env->ps, env->ds.ratio, env->E, env->day_finished ? 1 : 0, 1, st));
     env->p.packed = 0;   // word + f64 aux planes
     env->p.req_zero = 0;
     env->p.bump_day = 0;
     HIP_TRY(env, sng::launch_profiles(env->p, env->ds, env->E, st));
     // (the t = 0 penalty of a generated day is 0: observe0 writes it)
+    // (the PV ratio from each env's Python stream, after the owed day-end draw, inside observe0_kernel)
     HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, aligned16(obs) ? 1 : 0, st, OBS0_GENERATED,
-                                      -1));
+                                      -1, &env->ps, 1 | (env->day_finished ? 2 : 0)));
     // the next day's blocks of both streams, on the side stream, while this day is stepped
     // (mt_prepare_kernel: about every other day twists a numpy block, ~0.1 ms at 65,536 envs, off the next
     // reset's critical path); queued behind the t = 0 observation, which it would otherwise slow down
@@ -1178,10 +1178,10 @@ int sng_reset_replay(SngEnv *env, float *obs, void *stream) {
         if (rc) return rc;
         rc = await_prepare(env, st);
         if (rc) return rc;
-        HIP_TRY(env, launch_py_ratio(env->ps, env->ds.ratio, env->E, env->day_finished ? 1 : 0, 1, st));
         env->p.req_zero = 1;
         env->p.bump_day = 0;
-        HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, vec, st, OBS0_REPLAY, -1));
+        HIP_TRY(env, sng::launch_observe0(env->p, env->ds, obs, nullptr, env->E, vec, st, OBS0_REPLAY, -1, &env->ps,
+                                          1 | (env->day_finished ? 2 : 0)));
     } else {
         env->p.req_zero = 1;
         env->p.bump_day = 0;

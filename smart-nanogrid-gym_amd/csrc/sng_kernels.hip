@@ -1438,6 +1438,42 @@ __device__ __forceinline__ double replay_ratio_draw(uint64_t seed, uint64_t ge, 
 }
 
 // ---------------------------------------------------------------------------------
+// One env's Python `random` stream (RefStreams, tempered words, two blocks) on its lane: the day-end
+// random.randint(0, 180) the last step owes (end_draw; smart_nanogrid_environment.py:181) and the
+// reset's random.randint(0, 180) / 100 (draw; :349) -- _randbelow(181) as getrandbits(8) rejection.
+// A block boundary without a ready successor is twisted on the lane (mt_twist_lane).  Returns the
+// ratio (or `keep` when nothing is drawn) and stores the stream's new position.
+// ---------------------------------------------------------------------------------
+__device__ __noinline__ void mt_twist_lane(const uint32_t *A, uint32_t *B);
+__device__ __forceinline__ double py_ratio_lane(const RefStreams &ps, int64_t e, bool end_draw, bool draw,
+                                                double keep) {
+    uint32_t *blk = ps.mt + (size_t)e * 2 * kMtN;
+    const int32_t pos = ps.pos[e];
+    int cur = (pos >> 16) & 1, mti = pos & kMtPosMask;
+    bool ready = (pos & kMtNextReady) != 0;
+    auto next = [&]() -> uint32_t {
+        if (mti >= kMtN) {
+            if (!ready) mt_twist_lane(blk + cur * kMtN, blk + (cur ^ 1) * kMtN);
+            cur ^= 1;
+            mti -= kMtN;
+            ready = false;
+        }
+        return blk[cur * kMtN + mti++];   // tempered in HBM
+    };
+    auto randint180 = [&]() -> int {
+        uint32_t r;
+        do {
+            r = next() >> 24;
+        } while (r >= 181u);
+        return (int)r;
+    };
+    if (end_draw) (void)randint180();
+    const double ratio = draw ? (double)randint180() / 100 : keep;
+    ps.pos[e] = (cur << 16) | (ready ? kMtNextReady : 0) | mti;
+    return ratio;
+}
+
+// ---------------------------------------------------------------------------------
 // Observation at t = 0 after a reset (SmartNanogridEnv.reset -> __get_observations,
 // smart_nanogrid_environment.py:349-351): SOC[c, 0] as generated, departure times at 0.
 // mode (Obs0Mode, sng_layout.h) says where the PV ratio comes from and who advances the day
@@ -1446,7 +1482,7 @@ __device__ __forceinline__ double replay_ratio_draw(uint64_t seed, uint64_t ge, 
 template <int BLOCK, bool PK>
 __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s, float *__restrict__ obs,
                                                          double *__restrict__ ep_return, int64_t E, int vec_io,
-                                                         int mode, int64_t replay) {
+                                                         int mode, int64_t replay, RefStreams ps, int py) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int n = p.n, O = p.obs_dim;
     const int tid = threadIdx.x;
@@ -1457,7 +1493,13 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
     if (tid < nblk) {
         const uint64_t ge = (uint64_t)(e + p.env_offset);
         double ratio;
-        if (mode == OBS0_DEVICE) {   // the day's draw, as the fused generator's t = 0 blocks make it
+        if (py) {   // reference-RNG days: the Python stream's draws (py bit 0: the ratio, bit 1: the day-end draw)
+            ratio = py_ratio_lane(ps, e, (py & 2) != 0, (py & 1) != 0, 0.0);
+            if (py & 1)
+                s.ratio[e] = ratio;
+            else
+                ratio = s.ratio[e];
+        } else if (mode == OBS0_DEVICE) {   // the day's draw, as the fused generator's t = 0 blocks make it
             ratio = pv_ratio_draw(p.seed, ge, *s.episode);
             s.ratio[e] = ratio;
         } else if (mode == OBS0_REPLAY && replay >= 0) {
@@ -2104,17 +2146,21 @@ int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) 
 }
 
 hipError_t launch_observe0(const Params &p, const DeviceState &s, float *obs, double *ep_return, int64_t E,
-                           int vec_io, hipStream_t stream, int mode, int64_t replay) {
+                           int vec_io, hipStream_t stream, int mode, int64_t replay, const RefStreams *ps = nullptr,
+                           int py = 0) {
+    const RefStreams no_streams{nullptr, nullptr};
+    const RefStreams &pss = (py && ps) ? *ps : no_streams;
+    if (!ps) py = 0;
     if ((size_t)round4(256 * p.obs_dim) * 4 <= 64 * 1024) {
         const dim3 grid((unsigned)((E + 255) / 256)), block(256);
         auto kern = p.packed ? observe0_kernel<256, true> : observe0_kernel<256, false>;
         hipLaunchKernelGGL(kern, grid, block, (size_t)round4(256 * p.obs_dim) * 4, stream, p, s, obs, ep_return, E,
-                           vec_io, mode, replay);
+                           vec_io, mode, replay, pss, py);
     } else {
         const dim3 grid((unsigned)((E + kWave - 1) / kWave)), block(kWave);
         auto kern = p.packed ? observe0_kernel<kWave, true> : observe0_kernel<kWave, false>;
         hipLaunchKernelGGL(kern, grid, block, (size_t)round4(kWave * p.obs_dim) * 4, stream, p, s, obs, ep_return, E,
-                           vec_io, mode, replay);
+                           vec_io, mode, replay, pss, py);
     }
     return hipGetLastError();
 }
@@ -2810,50 +2856,6 @@ hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStream
     return hipGetLastError();
 }
 
-// ---------------------------------------------------------------------------------
-// The reference's Python `random` stream of every env on the device (random.seed(seed + global env),
-// CPython's MT19937; seeded on the host with init_by_array, sng_mt.h, and uploaded once): the PV ratio
-// random.randint(0, 180) / 100 of a reset (smart_nanogrid_environment.py:349), after the day-end draw
-// the last step still owes (:181).  RefStreams layout (two blocks per env, mt_prepare_kernel keeps the
-// successor ready); a block boundary without a ready successor is twisted on the lane.
-// Thread = env.  end_draw: consume the owed day-end randint first; draw: write ratio[e].
-// ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void py_ratio_kernel(RefStreams ps, double *__restrict__ ratio, int64_t E,
-                                                       int end_draw, int draw) {
-    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (e >= E) return;
-    uint32_t *blk = ps.mt + (size_t)e * 2 * kMtN;
-    const int32_t pos = ps.pos[e];
-    int cur = (pos >> 16) & 1, mti = pos & kMtPosMask;
-    bool ready = (pos & kMtNextReady) != 0;
-    auto next = [&]() -> uint32_t {
-        if (mti >= kMtN) {
-            if (!ready) mt_twist_lane(blk + cur * kMtN, blk + (cur ^ 1) * kMtN);
-            cur ^= 1;
-            mti -= kMtN;
-            ready = false;
-        }
-        return blk[cur * kMtN + mti++];   // tempered in HBM
-    };
-    auto randint180 = [&]() -> int {   // random.randint(0, 180): _randbelow(181), getrandbits(8) rejection
-        uint32_t r;
-        do {
-            r = next() >> 24;
-        } while (r >= 181u);
-        return (int)r;
-    };
-    if (end_draw) (void)randint180();
-    if (draw) ratio[e] = (double)randint180() / 100;
-    ps.pos[e] = (cur << 16) | (ready ? kMtNextReady : 0) | mti;
-}
-
-hipError_t launch_py_ratio(const RefStreams &ps, double *ratio, int64_t E, int end_draw, int draw,
-                           hipStream_t stream) {
-    if (!end_draw && !draw) return hipSuccess;
-    hipLaunchKernelGGL(py_ratio_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), 0, stream, ps, ratio, E,
-                       end_draw, draw);
-    return hipGetLastError();
-}
 
 __global__ void bump_day_kernel(DeviceState s) { *s.episode += 1; }
 
