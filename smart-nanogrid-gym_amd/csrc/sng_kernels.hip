@@ -1904,29 +1904,39 @@ hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, 
 }
 
 // ---------------------------------------------------------------------------------
-// The reference's rule-based controller (solvers/RBC/rbc.py:6-29), one thread per action entry
-// (coalesced action stores; an env's departure entries are adjacent).  Comparisons and the average in
-// float32, as numpy does on the float32 observation with a Python-float threshold (NEP 50).
+// The reference's rule-based controller (solvers/RBC/rbc.py:6-29): 256 envs per block, thread = env.
+// The block's observation rows (one contiguous run) come in through LDS with 16 B loads, the actions
+// leave through LDS with 16 B stores, as the step kernel stages its tiles.  Comparisons and the
+// average in float32, as numpy does on the float32 observation with a Python-float threshold (NEP 50).
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rbc_kernel(const float *__restrict__ obs, float *__restrict__ act,
-                                                  uint32_t total, uint32_t N, uint32_t A, uint32_t O) {
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    if (i >= total) return;
-    const uint32_t e = i / A, j = i - e * A;
-    float a = 0.f;   // the BESS entry, and an empty charger
-    if (j < N) {
-        const float *o = obs + (size_t)e * O;
-        const float d = o[8u + N + j];
-        a = (d == 0.f) ? 0.f : (d > 0.f && d < 0.16667f) ? 1.f : (o[0] + o[2]) / 2.f;
+__global__ __launch_bounds__(256) void rbc_kernel(const float *__restrict__ obs, float *__restrict__ act, int64_t E,
+                                                  int N, int A, int O, int vec_io) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    float *s_obs = lds, *s_act = lds + round4(256 * O);
+    const int tid = threadIdx.x;
+    const int64_t e0 = (int64_t)blockIdx.x * 256;
+    const int nblk = (int)((E - e0) < 256 ? (E - e0) : 256);
+    copy_in<8, 256>(s_obs, obs + e0 * O, nblk * O, vec_io != 0, tid);
+    __syncthreads();
+    if (tid < nblk) {
+        const float *o = s_obs + tid * O;
+        float *a = s_act + tid * A;
+        const float follow = (o[0] + o[2]) / 2.f;
+        for (int c = 0; c < N; ++c) {
+            const float d = o[8 + N + c];
+            a[c] = (d == 0.f) ? 0.f : (d > 0.f && d < 0.16667f) ? 1.f : follow;
+        }
+        if (A > N) a[N] = 0.f;   // the BESS action
     }
-    act[i] = a;
+    __syncthreads();
+    copy_out<256>(act + e0 * A, s_act, nblk * A, vec_io != 0, tid);
 }
 
 hipError_t launch_rbc(const float *obs, float *act, int64_t E, int N, int bess, hipStream_t stream) {
-    const uint32_t A = (uint32_t)(N + (bess ? 1 : 0)), O = (uint32_t)(2 * N + 8 + (bess ? 1 : 0));
-    const uint32_t total = (uint32_t)E * A;
-    hipLaunchKernelGGL(rbc_kernel, dim3((total + 255u) / 256u), dim3(256), 0, stream, obs, act, total, (uint32_t)N, A,
-                       O);
+    const int A = N + (bess ? 1 : 0), O = 2 * N + 8 + (bess ? 1 : 0);
+    const size_t lds = (size_t)(round4(256 * O) + round4(256 * A)) * 4;
+    const int vec = ((reinterpret_cast<uintptr_t>(obs) | reinterpret_cast<uintptr_t>(act)) & 15) == 0;
+    hipLaunchKernelGGL(rbc_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), lds, stream, obs, act, E, N, A, O, vec);
     return hipGetLastError();
 }
 

@@ -50,7 +50,7 @@ def main():
         obs = venv.reset_tensors()
         for _ in range(T):
             obs, rew, _ = venv.step_tensors(ctl(obs))
-            total.add_(rew)
+        total.add_(venv.return_d)   # the day's returns, accumulated by the step kernel
 
     def timed(run, days):
         for _ in range(args.warmup):
