@@ -2229,7 +2229,7 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
 //   mt_seed_kernel     init_genrand per env (once per seeding)
 //   mt_prepare_kernel  per env, one wavefront: the state one twist ahead into the other block (the
 //                      twist's three dependent ranges, 64 words at a time, in LDS)
-//   ref_day_kernel     per env, one thread: the day's draws and its timeline
+//   ref_day2_kernel    per env, one lane: the day's draws (phase 1) and its timeline (phase 2)
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t mt_temper(uint32_t y) { return mt_temper_word(y); }
 __device__ __forceinline__ uint32_t mt_untemper(uint32_t y) { return mt_untemper_word(y); }
@@ -2333,7 +2333,7 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
     if (lane == 0) rs.pos[e] = (cur << 16) | kMtNextReady | mti;
 }
 
-// One env's numpy stream inside ref_day_kernel: RandomState.random_sample / uniform / randint
+// One env's numpy stream inside ref_day2_kernel: RandomState.random_sample / uniform / randint
 // (legacy, masked rejection) over the tempered words of the prepared blocks (sng_mt.h, host twin).
 //
 // The words reach the lane through a ring of 128 words in LDS, topped up for the whole wavefront at
@@ -2354,14 +2354,6 @@ __device__ __forceinline__ double rand53(uint32_t wa, uint32_t wb) {
     const int32_t a = (int32_t)(wa >> 5), b = (int32_t)(wb >> 6);
     return (a * 67108864.0 + b) / 9007199254740992.0;
 }
-// Envs per wavefront (lanes >= kRefEnvs mirror lane % kRefEnvs: same stream, same branches, nothing
-// stored).  64 at 65,536 envs: 32 / 16 / 8 envs per wavefront ran the day in 338 / 405 / 505 us against
-// 331 us (rocprof, one box) -- the kernel is bound by the instructions the divergent wavefronts issue,
-// not by the latency more wavefronts would hide; at 4,096 envs 8 per wavefront is faster (193 vs 277 us).
-#ifndef SNG_REF_ENVS
-#define SNG_REF_ENVS 64
-#endif
-constexpr int kRefEnvs = SNG_REF_ENVS;
 template <int ENVS>
 struct MtRingT {
     uint32_t *blk;
@@ -2478,92 +2470,16 @@ struct MtRingT {
         return (((cur0 + k) & 1) << 16) | (k + 1 < avail ? kMtNextReady : 0) | (head - k * kMtN);
     }
 };
-using MtRing = MtRingT<kRefEnvs>;
-
-// The day of every env: generate_day + encode_day (sng_api.cpp) on one thread per env, charger by
-// charger; the lanes of a wavefront step (charger, t) together, so the timeline stores coalesce.
-constexpr int kRefBlock = kWave;   // one wavefront per workgroup, kRefEnvs envs: its rings are kRefEnvs x 512 B of LDS
-__global__ __launch_bounds__(kRefBlock) void ref_day_kernel(Params p, DeviceState s, RefStreams rs, int64_t E, int i4,
-                                                            int i10, int i1) {
-    __shared__ uint32_t rings[kRing * kRefEnvs];
-    const int lane = threadIdx.x % kRefEnvs;   // the env slot; lanes >= kRefEnvs mirror it
-    const int64_t e0 = (int64_t)blockIdx.x * kRefEnvs;
-    const bool live = e0 + lane < E && (int)threadIdx.x < kRefEnvs;
-    const int64_t e = e0 + lane < E ? e0 + lane : E - 1;   // past E: env E - 1's stream, nothing stored
-    const int32_t pos = rs.pos[e];
-    const int mti = pos & kMtPosMask;
-    MtRing rng{rs.mt + (size_t)e * 2 * kMtN, rings + lane, (pos >> 16) & 1, mti, mti & ~3, mti, 2};
-    const int T = p.T, n = p.n;
-    const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;   // as generate_kernel
-    const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
-                              : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
-    const uint32_t el4 = (uint32_t)e * 4u, el8 = (uint32_t)e * 8u;
-    for (int c = 0; c < n; ++c) {
-        const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
-        bool present = false, prev_occ = false;
-        int dep = 0, prev_rem = 0;
-        uint32_t cur_cap = 0;
-        double cur_req = 0.0, prev_req = 0.0;
-        for (int t = 0; t < T; ++t) {
-            rng.top_up();   // wave-uniform
-            bool arrived = false;
-            double soc_arr = 0.0;
-            if (!present) {
-#ifdef SNG_RD_NODRAW   // diagnostic builds only (timing breakdown of this kernel): no stream draws
-                const double r = (double)((e * 2654435761u + c * 97u + t * 31u) & 1023u) / 1024.0;
-                if ((r - 0.1) > 0.5) {
-                    present = arrived = true;
-                    soc_arr = 0.5;
-                    cur_cap = 40u;
-                    dep = t + i4 + 1;
-                }
-#else
-                const double r = rng.random();
-                if ((r - 0.1) > 0.5) {   // round(random.rand() - 0.1) == 1 (charging_station.py:214-215)
-                    present = arrived = true;
-                    soc_arr = rng.uniform(0.1, 0.9);                            // :257-259
-                    const double lo = soc_arr <= 0.9 ? soc_arr + 0.1 : 1.0;
-                    rng.skip2();                                                // discarded uniform, :219
-                    cur_cap = p.diff_caps ? (uint32_t)rng.randint(15, 120) : 40u;   // :267-269
-                    cur_req = p.req_enabled ? rng.uniform(lo, 1.0) : 1.0;       // :261-265
-                    const int high = min(t + i10, T + i1), low = t + i4;       // :271-279
-                    dep = (low >= high) ? low : rng.randint(low, high);
-                }
-#endif
-            }
-            const bool occ = present && t < dep;
-            if (!occ) present = false;
-            // encode_day: STATIC unless the running SoC carries over (occupied at t-1, no arrival)
-            const bool running = !arrived && prev_occ;
-            const int rem = occ ? dep - t : 0;
-            const bool pen = (uint32_t)prev_rem - pen_lo <= pen_span;   // prev_rem = 0: empty at t-1
-            const size_t plane = (size_t)t * n * (size_t)E;
-#ifdef SNG_RD_NOSTORE   // diagnostic builds only: the day's draws without its timeline stores
-            if (live && soc_arr == 12345.0) {
-#else
-            if (live) {
-#endif
-                bst(s.word + plane, el4, pack_word(occ, !running, pen, occ ? cur_cap : 0u, (uint32_t)rem), r4);
-                bst(s.aux + plane, el8, (occ && !running) ? soc_arr : 0.0, r8);
-                // Requested_SOC[c, t-1]; slot 0 holds Requested_SOC[c, T-1] (written after the loop)
-                if (p.req_stream && t > 0) bst(s.req + plane, el8, prev_req, r8);
-            }
-            prev_occ = occ;
-            prev_rem = rem;
-            prev_req = occ ? cur_req : 0.0;
-        }
-        if (live && p.req_stream) bst(s.req, el8, prev_req, r8);
-    }
-    if (live) rs.pos[e] = rng.position();
-}
+// One wavefront per workgroup; ENVS envs per wavefront (ref_day2_envs), the other lanes mirroring them.
+constexpr int kRefBlock = kWave;
 
 // The same day in two phases per charger, as generate_kernel draws a device day: (1) the charger's
 // vehicles, visiting only the steps that draw (a free step draws the arrival test, an arrival the
 // vehicle's values; an occupied step and a departure step draw nothing, charging_station.py:200-279),
 // into a per-lane list in LDS; (2) the word / f64 aux (/ req) timeline from the list, branch-free, step
-// by step.  The steps-major loop above executed the arrival path under a mask in nearly every (charger,
+// by step.  Round 2's steps-major kernel executed the arrival path under a mask in nearly every (charger,
 // step) iteration of a wavefront; here a wavefront iterates once per draw step of its busiest lane
-// (about 5 of a charger's 24 steps draw).  The stream is consumed draw for draw as above.
+// (about 5 of a charger's 24 steps draw).  The stream is consumed draw for draw.
 constexpr int kRefVeh = 8;   // vehicles per charger-day (T / (4/dt + 1) + 1 <= 7 for every dt dividing 24 h) + sentinel
 // Phase 1 reads each draw step's words from the ring in two batches of LDS reads instead of one round
 // trip per word: after a top_up every lane still drawing holds more than kRing / 4 words, so the 10 words
@@ -2850,10 +2766,6 @@ hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStream
         hipError_t e = launch_mt_prepare(rs, E, stream);
         if (e != hipSuccess) return e;
     }
-#ifdef SNG_REF_STEPS   // A/B builds: the steps-major kernel
-    const dim3 grid((unsigned)((E + kRefEnvs - 1) / kRefEnvs)), block(kRefBlock);
-    hipLaunchKernelGGL(ref_day_kernel, grid, block, 0, stream, p, s, rs, E, i4, i10, i1);
-#else
     const bool req = p.req_stream != 0;
     if (p.T == 24) {
         if (req) launch_ref_day2<24, true>(p, s, rs, E, i4, i10, i1, stream);
@@ -2862,7 +2774,6 @@ hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStream
         if (req) launch_ref_day2<0, true>(p, s, rs, E, i4, i10, i1, stream);
         else launch_ref_day2<0, false>(p, s, rs, E, i4, i10, i1, stream);
     }
-#endif
     return hipGetLastError();
 }
 

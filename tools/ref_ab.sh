@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out; mkdir -p $OUT
-LIBS="${AB_LIBS:-libsng_refsteps libsng}"
+LIBS="${AB_LIBS:-libsng}"
 for l in $LIBS; do
   SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so timeout -k 10 600 python -u -m pytest -q -x --timeout 300 --timeout-method thread \
     tests/test_gpu_parity.py -k "golden or batched_reference or many_days or full_size_sampled or config5_extended or sharded" \
