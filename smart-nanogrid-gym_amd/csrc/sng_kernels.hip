@@ -1904,19 +1904,21 @@ hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, 
 }
 
 // ---------------------------------------------------------------------------------
-// The reference's rule-based controller (solvers/RBC/rbc.py:6-29): 256 envs per block, thread = env.
+// The reference's rule-based controller (solvers/RBC/rbc.py:6-29): 256 (wide stations: 64) envs per block,
+// thread = env.
 // The block's observation rows (one contiguous run) come in through LDS with 16 B loads, the actions
 // leave through LDS with 16 B stores, as the step kernel stages its tiles.  Comparisons and the
 // average in float32, as numpy does on the float32 observation with a Python-float threshold (NEP 50).
 // ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void rbc_kernel(const float *__restrict__ obs, float *__restrict__ act, int64_t E,
-                                                  int N, int A, int O, int vec_io) {
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void rbc_kernel(const float *__restrict__ obs, float *__restrict__ act, int64_t E,
+                                                    int N, int A, int O, int vec_io) {
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    float *s_obs = lds, *s_act = lds + round4(256 * O);
+    float *s_obs = lds, *s_act = lds + round4(BLOCK * O);
     const int tid = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * 256;
-    const int nblk = (int)((E - e0) < 256 ? (E - e0) : 256);
-    copy_in<8, 256>(s_obs, obs + e0 * O, nblk * O, vec_io != 0, tid);
+    const int64_t e0 = (int64_t)blockIdx.x * BLOCK;
+    const int nblk = (int)((E - e0) < BLOCK ? (E - e0) : BLOCK);
+    copy_in<8, BLOCK>(s_obs, obs + e0 * O, nblk * O, vec_io != 0, tid);
     __syncthreads();
     if (tid < nblk) {
         const float *o = s_obs + tid * O;
@@ -1929,14 +1931,21 @@ __global__ __launch_bounds__(256) void rbc_kernel(const float *__restrict__ obs,
         if (A > N) a[N] = 0.f;   // the BESS action
     }
     __syncthreads();
-    copy_out<256>(act + e0 * A, s_act, nblk * A, vec_io != 0, tid);
+    copy_out<BLOCK>(act + e0 * A, s_act, nblk * A, vec_io != 0, tid);
 }
 
 hipError_t launch_rbc(const float *obs, float *act, int64_t E, int N, int bess, hipStream_t stream) {
     const int A = N + (bess ? 1 : 0), O = 2 * N + 8 + (bess ? 1 : 0);
-    const size_t lds = (size_t)(round4(256 * O) + round4(256 * A)) * 4;
     const int vec = ((reinterpret_cast<uintptr_t>(obs) | reinterpret_cast<uintptr_t>(act)) & 15) == 0;
-    hipLaunchKernelGGL(rbc_kernel, dim3((unsigned)((E + 255) / 256)), dim3(256), lds, stream, obs, act, E, N, A, O, vec);
+    const size_t lds256 = (size_t)(round4(256 * O) + round4(256 * A)) * 4;
+    if (lds256 <= 64 * 1024) {   // up to 20 chargers
+        hipLaunchKernelGGL(rbc_kernel<256>, dim3((unsigned)((E + 255) / 256)), dim3(256), lds256, stream, obs, act, E, N,
+                           A, O, vec);
+    } else {                     // wide stations: 64-env tiles (100 KB at the ABI's 128 chargers)
+        const size_t lds64 = (size_t)(round4(64 * O) + round4(64 * A)) * 4;
+        hipLaunchKernelGGL(rbc_kernel<64>, dim3((unsigned)((E + 63) / 64)), dim3(64), lds64, stream, obs, act, E, N, A,
+                           O, vec);
+    }
     return hipGetLastError();
 }
 

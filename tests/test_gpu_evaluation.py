@@ -93,7 +93,7 @@ def test_evaluate_models_same_days(rng):
     assert mean["full"] != mean["zeros"]
 
 
-@pytest.mark.parametrize("N,bess", [(4, True), (10, True), (10, False), (50, True)])
+@pytest.mark.parametrize("N,bess", [(4, True), (10, True), (10, False), (50, True), (128, False)])
 def test_native_rule_based_controller_equals_rbc(N, bess):
     """sng_rule_based_actions (the controller's device path) against the controller's torch restatement of
     solvers/RBC/rbc.py:6-29 on the CPU, bit for bit: departure entries exactly 0, at and around the
