@@ -35,7 +35,8 @@ for s in $STEPS; do
     prof)  run prof_stats 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline ;;
     cfg5)  run bench_cfg5 600 python bench.py --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 --cpu-budget 12
            run prof_cfg5 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_cfg5 -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 ;;
-    closed) run closed_loop 600 python tools/closed_loop_bench.py ;;
+    closed) run closed_loop 600 python tools/closed_loop_bench.py
+            run closed_loop_mlp 600 python tools/closed_loop_bench.py --policy mlp ;;
     memfloor) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_memfloor.so run memfloor 300 python bench.py --no-cpu-baseline
            SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_memfloor.so run memfloor_cfg5 300 python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 ;;
     reset) run reset_bench 600 python tools/reset_bench.py ;;
