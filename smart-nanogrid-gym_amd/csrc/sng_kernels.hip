@@ -1750,7 +1750,10 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 // at 65,536 x 10 (A/B, one box), the steps' code and state staying in L2.  Diagnostic builds
 // (tools/gpu_session.sh ablib) split the reset's time: without the t = 0 observation blocks 24.3-24.9 us
 // (they run beside the timeline blocks), without phase 1's draws 20.7, without the record stores 16-16.8.
-constexpr int kGenRecPol = kNT;
+#ifndef SNG_GEN_POL
+#define SNG_GEN_POL kNT
+#endif
+constexpr int kGenRecPol = SNG_GEN_POL;
 // Vehicle list entries (LDS) are kept in the record's own layout: arrival step in bits 0-7 (the flag
 // bits of a record, masked off), capacity in 8-15 and departure step in 16-23, so an occupied step's
 // record is (entry & 0xffff00 | flags) - t << 16 (the departure field becomes the steps left; it is
