@@ -1750,6 +1750,8 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 // at 65,536 x 10 (A/B, one box), the steps' code and state staying in L2.  Diagnostic builds
 // (tools/gpu_session.sh ablib) split the reset's time: without the t = 0 observation blocks 24.3-24.9 us
 // (they run beside the timeline blocks), without phase 1's draws 20.7, without the record stores 16-16.8.
+// SNG_GEN_POL: A/B builds only.  Write-through record stores (sc1 | nt, sc0 | sc1 | nt) left the day
+// and the reset unchanged (profiles/r03_ab_generator_store_policy.txt).
 #ifndef SNG_GEN_POL
 #define SNG_GEN_POL kNT
 #endif
