@@ -834,8 +834,16 @@ __device__ __forceinline__ double from_part(double x) {
 // fewer than 8 powers are numpy's in-order sum when one lane holds them all), the first lane adds the
 // other lanes' vehicle penalties after its own in charger order (Python's sum, penaliser.py:55), and the
 // rare exact-order paths run on the first lane over all chargers.
+// Waves per SIMD the register budget is sized for: L by default (every wave of the E = 65,536 grid resident
+// at once); SNG_WIDE_WPE (A/B builds) caps it.  Config 5 with four lanes per env and a 3-wave budget (166
+// VGPRs, no spills, 3 of the 4,096 waves per SIMD resident): 29.6-29.8 us against 23.4 us with two lanes
+// (profiles/r03_ab_config5_four_lanes.txt).
+#ifndef SNG_WIDE_WPE
+#define SNG_WIDE_WPE 4
+#endif
 template <int NC, int L, bool PK, bool REQ, bool NOISE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(L, L))) void step_wide_kernel(
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(L < SNG_WIDE_WPE ? L : SNG_WIDE_WPE,
+                                                                      L < SNG_WIDE_WPE ? L : SNG_WIDE_WPE))) void step_wide_kernel(
     const float *__restrict__ act, float *__restrict__ obs, double *__restrict__ reward, uint8_t *__restrict__ done,
     int64_t E, int t, int vec_io, StepConst k, Params p, DeviceState s, InfoPtrs info) {
     static_assert(L == 1 || L == 2 || L == 4, "one, two or four lanes per env");
