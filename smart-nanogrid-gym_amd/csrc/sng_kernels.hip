@@ -798,7 +798,10 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
 #ifndef SNG_WIDE_SB
 #define SNG_WIDE_SB 1
 #endif
-constexpr int kWideSB = SNG_WIDE_SB;   // chargers per scheduling group of the wide kernel's fast loop
+// chargers per scheduling group of the wide kernel's fast loop.  A/B (profiles/r03_ab_wide_sched_groups.txt):
+// config 5 22.6-22.7 us at 1 and 2, 22.8 at 5, 27.1 with no barrier in a lane's 25 chargers; the headline
+// within noise
+constexpr int kWideSB = SNG_WIDE_SB;
 
 template <int NC, int L>
 struct WideLds {
