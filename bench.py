@@ -20,12 +20,13 @@ dispatch time of the step kernel (`eager_launch_us`, `frac_eager`) come from HIP
 attached to every dispatch of eager days right after the timed region, on the stream the kernels run on.
 `frac_rocprof` is the same bytes over the average duration of that kernel in the committed
 rocprofv3 --kernel-trace --stats summary (profiles/), when one exists for this kernel.  Beside the
-SURVEY.md 8(d) fraction: `frac_layout` prices the bytes this layout actually moves (32N + 89 B per env-step,
-+4 B for the error flags the default SngInfo writes), `frac_pmc` the PMC-measured HBM bytes (`traffic`,
+SURVEY.md 8(d) fraction: `frac_layout` prices the bytes this layout actually moves (32N + 89 B per env-step;
++4 B with --per-env-flags), `frac_pmc` the PMC-measured HBM bytes (`traffic`,
 from the committed passes, null if absent), and `copy_step_size` / `copy_1gib` are the measured ceiling
 SURVEY.md 8(d) asks for: libsng's float4 copy probe (sng_bandwidth_probe) moving the step's own read and
-write bytes in one dispatch, and 1 GiB.  The step is timed with the default SngInfo (flag store on;
---no-flags times it without).  `cpu_baseline` is the C restatement of the reference's step()/reset()
+write bytes in one dispatch, and 1 GiB.  The step is timed with the default SngInfo of
+SmartNanogridVecEnv: the day return and the flag summary word (touched only when an env raises a flag);
+--per-env-flags adds the per-step per-env flag store the diagnostics use.  `cpu_baseline` is the C restatement of the reference's step()/reset()
 (oracle/, kind "port", label "restatement") run as one process per host core granted by the cgroup CPU
 quota (sched_getaffinity shows the whole machine on a GPU box), measured before the GPU is touched, with
 the reference's own Python step() range from SURVEY.md section 6 beside it.
@@ -56,12 +57,13 @@ def survey_bytes(n):
     return 40 * n + 65
 
 
-def step_kernel_bytes(n, noise=False, flags=True):
+def step_kernel_bytes(n, noise=False, flags=False):
     """What this layout moves per env-step of a device-RNG day (b-pv, no requested-SoC stream), as
     (read, written): reads = actions 4(N+1) + packed 4-byte charger-step record 4N (sng_layout.h) + EV SoC
     8N + BESS 8 + PV ratio 8 + day return 8 (+ 64 for the PV / price profile factors of t..t+3 with
     stochastic profiles); writes = obs 4(2N+9) + reward 8 + done 1 + EV SoC 8N + BESS 8 + day return 8
-    (+ 4 for the per-env error flags the default SngInfo passes).  32N + 89 (+4) in all.  Host-RNG days
+    (+ 4 for the per-env per-step error flags, flags=True: the diagnostics' SngInfo.flags; the default
+    SngInfo watches the one-word flag summary instead).  32N + 89 (+4) in all.  Host-RNG days
     read the word and a float64 static SoC instead: 40N + 89."""
     rd = 4 * (n + 1) + 4 * n + 8 * n + 8 + 8 + 8 + (64 if noise else 0)
     wr = 4 * (2 * n + 9) + 8 + 1 + 8 * n + 8 + 8 + (4 if flags else 0)
@@ -217,8 +219,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: RCCL over xGMI (default), or gloo with the day returns staged through host "
                          "memory (several ranks on one GPU, tests)")
-    ap.add_argument("--no-flags", action="store_true",
-                    help="time the step without the per-env error-flag store (the default SngInfo keeps it)")
+    ap.add_argument("--per-env-flags", action="store_true",
+                    help="time the step with the per-env per-step error-flag store of the diagnostics (the default "
+                         "SngInfo watches the flag summary word instead)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -264,8 +267,8 @@ def main():
     acts = torch.where(torch.rand(acts.shape, generator=g, device=device) < 0.2, torch.zeros_like(acts), acts)
     acts = acts.contiguous()
     # the default SngInfo: the per-env error flags and the day return (for the all-gather), no diagnostics
-    if args.no_flags:
-        venv._info.flags = None
+    if args.per_env_flags:
+        venv._info.flags = venv.flags_d.data_ptr()
     venv.reset_tensors(rng="device")
     kernel = venv.step_kernel_name()   # the instantiation the graphs below launch (device-RNG days)
     # days per graph replay (the same at every N, so per-GPU work is identical)
@@ -343,7 +346,7 @@ def main():
         eager_s = float(np.mean(kernel_ms)) * 1e-3
         bpl = survey_bytes(N) * E
         achieved = bpl / launch_s / 1e9
-        rd, wr = step_kernel_bytes(N, noise, flags=not args.no_flags)
+        rd, wr = step_kernel_bytes(N, noise, flags=args.per_env_flags)
         lpl = (rd + wr) * E
         traffic = load_pmc_traffic(E, N, kernel)
         rp_us, rp_file = rocprof_average_us(kernel, args.extended_day or noise)
@@ -357,7 +360,7 @@ def main():
                 "kernel": kernel, "bytes_model": f"SURVEY.md 8(d) B(N) = 40N+65 = {survey_bytes(N)} B per env-step",
                 "bytes_per_launch": bpl,
                 "layout_bytes_model": f"this layout: {rd} B read + {wr} B written per env-step "
-                                      f"(bench.step_kernel_bytes; flag store {'off' if args.no_flags else 'on'})",
+                                      f"(bench.step_kernel_bytes; per-env flag store {'on' if args.per_env_flags else 'off'})",
                 "layout_bytes_per_launch": lpl,
                 "frac_layout": frac(lpl, launch_s),
                 "frac_pmc": None if traffic is None else frac(traffic, launch_s),

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 8
+#define SNG_ABI_VERSION 9
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -146,6 +146,11 @@ typedef struct SngInfo {
     /* per charger, [num_envs][N] (row-major, env-major); NULL = not written */
     double *charger_power;               /* 'Charger power values' (charging_station.py:282-299) */
     double *vehicle_soc;                 /* SOC[c, t] after the step (charger.py:37-56/:86/:136) */
+    /* device u32, NULL = not written: OR of the SNG_FLAG_* any env raised since the caller last zeroed it
+     * (one word, touched only when a flag is raised).  A caller that watches this word instead of `flags`
+     * spares the step its per-env flag store, and reads which envs raised what with
+     * sng_read_errors(clear = 1) only when the word is non-zero. */
+    uint32_t *flag_summary;
 } SngInfo;
 
 /* A scenario in the reference's own layout (ChargingStation after

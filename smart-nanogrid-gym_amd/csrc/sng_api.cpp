@@ -587,6 +587,7 @@ InfoPtrs info_ptrs(const SngInfo *i) {
     o.episode_return = i->episode_return;
     o.charger_power = i->charger_power;
     o.vehicle_soc = i->vehicle_soc;
+    o.flag_any = i->flag_summary;
     return o;
 }
 
@@ -616,8 +617,19 @@ int ensure_staging(SngEnv *env, bool with_req) {
 // (block 0, position N: the first draw twists), then drawn by observe0_kernel (py_ratio_lane): random.randint(0, 180)
 // for a reset's PV ratio, after the day-end draw the last step owes (smart_nanogrid_environment.py:181, 349).
 int await_prepare(SngEnv *env, hipStream_t st);
+// numpy's np.random.seed takes seeds in [0, 2^32): env i of a reference-RNG population is seeded
+// seed + env offset + i, so the last env's seed must stay below 2^32 (mt_seed_kernel would wrap it).
+int check_reference_seed(SngEnv *env) {
+    const uint64_t last = env->seed + (uint64_t)env->p.env_offset + (uint64_t)(env->E - 1);
+    if (env->seed >= (1ull << 32) || last >= (1ull << 32) || last < env->seed)
+        return fail(env, SNG_ERR_INVALID_ARGUMENT,
+                    "reference RNG: seed + env offset + env index must be < 2^32 (np.random.seed's range)");
+    return SNG_OK;
+}
+
 int ensure_py_streams(SngEnv *env, hipStream_t st) {
     const size_t E = (size_t)env->E;
+    if (int rc = check_reference_seed(env)) return rc;
     if (!env->ps.mt) {
         HIP_TRY(env, hipMalloc(&env->ps.mt, E * 2 * kMtN * sizeof(uint32_t)));
         HIP_TRY(env, hipMalloc(&env->ps.pos, E * sizeof(int32_t)));
@@ -656,6 +668,7 @@ int await_prepare(SngEnv *env, hipStream_t st) {
 
 // ... and numpy's on the device (mt_seed_kernel), queued on `st`.
 int ensure_np_streams(SngEnv *env, hipStream_t st) {
+    if (int rc = check_reference_seed(env)) return rc;
     if (!env->rs.mt) {
         HIP_TRY(env, hipMalloc(&env->rs.mt, (size_t)env->E * 2 * kMtN * sizeof(uint32_t)));
         HIP_TRY(env, hipMalloc(&env->rs.pos, (size_t)env->E * sizeof(int32_t)));
@@ -1492,7 +1505,9 @@ struct StateHeader {
     int32_t has_word, has_req, has_prof, has_return, has_streams, reserved;
     uint64_t total_bytes;
 };
-static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '2'};
+// the last byte is the checkpoint format version: '3' since the configuration fingerprint is hashed
+// field by field (round 3); a blob of another version is refused as such
+static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '3'};
 
 // The blob's size for this handle and the header's section flags.
 static uint64_t state_bytes(const SngEnv *env, const StateHeader &h) {
@@ -1611,6 +1626,10 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
     if (bytes < sizeof(StateHeader)) return fail(env, SNG_ERR_INVALID_ARGUMENT, "not an sng state");
     StateHeader h;
     std::memcpy(&h, buf, sizeof h);
+    if (std::memcmp(h.magic, kStateMagic, sizeof h.magic - 1) == 0 && h.magic[7] != kStateMagic[7])
+        return fail(env, SNG_ERR_INVALID_ARGUMENT,
+                    std::string("unsupported checkpoint version ") + h.magic[7] + " (this library reads version " +
+                        kStateMagic[7] + ")");
     if (std::memcmp(h.magic, kStateMagic, sizeof h.magic) != 0 || h.abi != SNG_ABI_VERSION ||
         h.header_bytes != (int32_t)sizeof(StateHeader))
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "not an sng state of this ABI version");

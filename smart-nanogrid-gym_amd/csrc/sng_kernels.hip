@@ -498,7 +498,10 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     // (the observation header was written before the chargers: step_kernel)
     if (p.bess) o_row[p.obs_dim - 1] = (float)bess;
 
-    if (fl) atomicOr(s.flags + e0 + lo, fl);   // rare (sticky error bits); no-return atomic, nothing waits
+    if (fl) {   // rare (sticky error bits); no-return atomics, nothing waits
+        atomicOr(s.flags + e0 + lo, fl);
+        if (info.flag_any) atomicOr(info.flag_any, fl);
+    }
     if (info.flags) bst(info.flags, el1 * 4u, fl);
     if (info.episode_return) bst<kNT>(info.episode_return, el8, ret_prev + -total);
     if (DIAG) {
@@ -844,215 +847,292 @@ __device__ __forceinline__ double from_part(double x) {
 #ifndef SNG_WIDE_WPE
 #define SNG_WIDE_WPE 4
 #endif
+// One group of WENVS envs of a wavefront: its loads (issue), then its step (run).  A wavefront steps G
+// groups: every group's loads are issued before the first group is stepped, so a group's arithmetic and
+// stores overlap the later groups' loads still in flight (G = 1: the whole wavefront is one group).
 template <int NC, int L, bool PK, bool REQ, bool NOISE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(L < SNG_WIDE_WPE ? L : SNG_WIDE_WPE,
-                                                                      L < SNG_WIDE_WPE ? L : SNG_WIDE_WPE))) void step_wide_kernel(
-    const float *__restrict__ act, float *__restrict__ obs, double *__restrict__ reward, uint8_t *__restrict__ done,
-    int64_t E, int t, int vec_io, StepConst k, Params p, DeviceState s, InfoPtrs info) {
-    static_assert(L == 1 || L == 2 || L == 4, "one, two or four lanes per env");
+struct WideGroup {
     using Lay = WideLds<NC, L>;
-    constexpr int WENVS = Lay::WENVS, CPL = (NC + L - 1) / L;
+    static constexpr int WENVS = Lay::WENVS, CPL = (NC + L - 1) / L;
+    static constexpr int KT = (Lay::A * WENVS + 4 * kWave - 1) / (4 * kWave);
     static_assert((L - 1) * CPL < NC, "every lane steps at least one charger");
-    constexpr int KT = (Lay::A * WENVS + 4 * kWave - 1) / (4 * kWave);
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int Ad = p.act_dim, O = p.obs_dim;
-    const int lane = threadIdx.x, le = lane / L, part = lane % L;
-    const bool leader = part == 0;
-    const int64_t e0 = (int64_t)blockIdx.x * WENVS;   // the grid covers E exactly: every wave has an env
-    const int nw = (E - e0) < WENVS ? (int)(E - e0) : WENVS;
-    const bool live = le < nw;
-    float *s_act = lds;
-    float *s_obs = lds + Lay::ACT;
-    const int64_t el = live ? e0 + le : E - 1;   // idle lanes load a valid env and discard it
-    const uint32_t el1 = (uint32_t)el, el4 = el1 * 4u, el8 = el1 * 8u;
-    const size_t plane = (size_t)t * NC * (size_t)E;   // this step's timeline planes
-    const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
-    const int c0 = part * CPL;
-    const int nc = (NC - c0) < CPL ? NC - c0 : CPL;   // the lane's chargers (the last lane's range is ragged)
-    // the lane's first charger row as a per-lane byte offset; charger j of the lane adds j * E (uniform).
-    // Past the lane's range (j >= nc) the loads re-read its first charger and nothing is stored.
-    const uint32_t row4 = el4 + (uint32_t)c0 * (uint32_t)E * 4u;
-    const uint32_t row4_last = el4 + (uint32_t)(NC - 1) * (uint32_t)E * 4u;
+    int64_t e0;
+    int nw;
+    bool live;
+    uint32_t el1, el4, el8, row4, row4_last;
+    TileStage<KT, kWave> act_tile;
+    double ratio, bess_l, pen0_l, ret_l;
+    double fpv[4], fpr[4];
+    uint32_t w[CPL];
+    double aux[PK ? 1 : CPL], run_[CPL], req[REQ ? CPL : 1];
+
     // the (per-lane, uniform) byte offsets of charger j of the lane: j * E in the uniform part, except for
     // the j some lane lacks (a ragged last lane), where the per-lane part carries it
-    auto ragged = [](int j) { return NC % L != 0 && j >= NC - (L - 1) * CPL; };
-    auto r4_of = [&](int j) -> uint32_t { return ragged(j) ? 0u : (uint32_t)j * (uint32_t)E * 4u; };
-    auto row_of = [&](int j) -> uint32_t {
+    static __device__ __forceinline__ bool ragged(int j) { return NC % L != 0 && j >= NC - (L - 1) * CPL; }
+    __device__ __forceinline__ uint32_t r4_of(int j, int64_t E) const {
+        return ragged(j) ? 0u : (uint32_t)j * (uint32_t)E * 4u;
+    }
+    __device__ __forceinline__ uint32_t row_of(int j, int nc, int64_t E) const {
         return ragged(j) ? (j < nc ? row4 + (uint32_t)j * (uint32_t)E * 4u : row4_last) : row4;
-    };
+    }
 
     // loads oldest-needed-first: the actions tile and the per-env values, then every charger's state
-    TileStage<KT, kWave> act_tile;
-    act_tile.issue(act + e0 * Ad, nw * Ad, vec_io != 0, lane);
-    const double ratio = bld(s.ratio, el8);
-    const double bess_l = bld(p.bess ? s.bess : s.ratio, el8);
-    const double pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
-    const double ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
-    double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
-    if constexpr (NOISE) {   // the day's profile factors of t..t+3 (profile_kernel)
-        const size_t pp = (size_t)(p.T + 3) * E;
+    __device__ __forceinline__ void issue(int64_t e0_, const float *act, int64_t E, int t, int vec_io, const Params &p,
+                                          const DeviceState &s, const InfoPtrs &info, int lane) {
+        const int le = lane / L, part = lane % L;
+        e0 = e0_;
+        nw = (E - e0) < WENVS ? (int)(E - e0) : WENVS;
+        live = le < nw;
+        const int64_t el = live ? e0 + le : E - 1;   // idle lanes load a valid env and discard it
+        el1 = (uint32_t)el;
+        el4 = el1 * 4u;
+        el8 = el1 * 8u;
+        const int c0 = part * CPL;
+        const int nc = (NC - c0) < CPL ? NC - c0 : CPL;
+        // the lane's first charger row as a per-lane byte offset; charger j of the lane adds j * E (uniform).
+        // Past the lane's range (j >= nc) the loads re-read its first charger and nothing is stored.
+        row4 = el4 + (uint32_t)c0 * (uint32_t)E * 4u;
+        row4_last = el4 + (uint32_t)(NC - 1) * (uint32_t)E * 4u;
+        const size_t plane = (size_t)t * NC * (size_t)E;   // this step's timeline planes
+        const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
+        const int Ad = p.act_dim;
+        act_tile.issue(act + e0 * Ad, nw * Ad, vec_io != 0, lane);
+        ratio = bld(s.ratio, el8);
+        bess_l = bld(p.bess ? s.bess : s.ratio, el8);
+        pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
+        ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            fpv[j] = bld(s.prof + (size_t)(t + j) * E, el8);
-            fpr[j] = bld(s.prof + pp + (size_t)(t + j) * E, el8);
-        }
-    }
-    uint32_t w[CPL];
-    double aux[PK ? 1 : CPL], run[CPL], req[CPL];
+        for (int j = 0; j < 4; ++j) fpv[j] = fpr[j] = 1.0;
+        if constexpr (NOISE) {   // the day's profile factors of t..t+3 (profile_kernel)
+            const size_t pp = (size_t)(p.T + 3) * E;
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-        // charger c0 + j (past a ragged lane's range: its charger NC - 1 again, discarded)
-        const uint32_t v4 = row_of(j), r4 = r4_of(j), v8 = 2u * v4, r8 = 2u * r4;
-        if (PK) {
-            w[j] = bld(rec_t, v4, r4);
-        } else {
-            w[j] = bld(s.word + plane, v4, r4);
-            aux[PK ? 0 : j] = bld(s.aux + plane, v8, r8);
-        }
-        run[j] = bld(s.soc, v8, r8);
-        req[j] = REQ ? bld(s.req + plane, v8, r8) : (p.req_zero ? 0.0 : 1.0);
-    }
-    act_tile.commit(s_act, lane);
-    wave_lds_fence();
-
-    const float *a_row = s_act + le * Ad;
-    float *o_row = s_obs + le * O;
-    float av[CPL];
-    float amin = 0.0f;
-#pragma unroll
-    for (int j = 0; j < CPL; ++j) {
-        av[j] = a_row[(c0 + j) < NC ? c0 + j : NC - 1];
-        amin = __builtin_fminf(amin, av[j]);   // a NaN action is not negative (fmin drops it)
-    }
-    const float bess_action = p.bess ? a_row[NC] : 0.0f;
-    const int k_soc = p.pv ? 8 : 4;
-    if (live && leader) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, fpv, fpr);
-
-    double pen_v = 0.0, p_ch = 0.0, p_dis = 0.0;
-    uint32_t n_nonexist = 0, fl = 0;
-    if (__builtin_amdgcn_ballot_w64(live && amin < 0.0f) == 0) {
-        // the fast loop: no negative action in the wave, so no negative power (p_dis stays 0.0)
-        double seq_pos = 0.0, pmin = __builtin_inf();
-        int n_pos = 0;
-        double qv[L > 1 ? CPL : 1];
-        if (live) {
-#pragma unroll
-            for (int j = 0; j < CPL; ++j) {
-                const int c = c0 + j;
-                if (NC % L != 0 && j >= nc) {   // a ragged lane's range ends: adds nothing
-                    qv[L > 1 ? j : 0] = 0.0;
-                    continue;
-                }
-                const uint32_t capi = (w[j] >> W_CAP_SHIFT) & 0xffu;
-                const bool occ = (w[j] & W_OCC) != 0;
-                const ChargerResult r = charger_step<true, true>(p, PK ? (w[j] & ~W_STATIC) : w[j],
-                                                                 PK ? 0.0 : aux[PK ? 0 : j], run[j], req[j], av[j], t,
-                                                                 recip_cap((double)capi));
-                bst<kNT>(s.soc, 2u * row_of(j), (PK && !occ) ? (double)rec_soc(w[j]) : r.soc, 2u * r4_of(j));
-                o_row[k_soc + c] = (float)r.soc;
-                o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[j]);
-                n_nonexist += r.nx;
-                fl |= r.fl;
-                if (L > 1) qv[L > 1 ? j : 0] = r.q;
-                pen_v += r.q;
-                const bool ip = r.pw > 0.0;
-                seq_pos += __builtin_fmax(r.pw, 0.0);
-                n_pos += ip ? 1 : 0;
-                pmin = __builtin_fmin(pmin, ip ? r.pw : __builtin_inf());
-                // chargers in order (groups of kWideSB): charger j waits only for its own loads
-                if ((j + 1) % kWideSB == 0) __builtin_amdgcn_sched_barrier(0);
+            for (int j = 0; j < 4; ++j) {
+                fpv[j] = bld(s.prof + (size_t)(t + j) * E, el8);
+                fpr[j] = bld(s.prof + pp + (size_t)(t + j) * E, el8);
             }
         }
-        // numpy sums fewer than 8 positive powers in order: one lane's running sum is that sum; two lanes'
-        // partial sums combined are that sum only when one of them is empty or the sum is exact
-        bool split = false;
-        if constexpr (L > 1) {
-            // the other lanes' totals (exact combinations), and their penalties after the first lane's own,
-            // in charger order (adding a +0.0 term is exact)
-            const double seq_own = seq_pos, pmin_own = pmin;
-            const int n_own = n_pos;
-            const uint32_t nx_own = n_nonexist, fl_own = fl;
-            int with_pos = n_own > 0 ? 1 : 0;
-            auto gather = [&](auto kc) {
-                constexpr int K = decltype(kc)::value;
-                const int nk = (int)from_part<L, K>((uint32_t)n_own);
-                with_pos += nk > 0 ? 1 : 0;
-                n_pos += nk;
-                seq_pos += from_part<L, K>(seq_own);
-                pmin = __builtin_fmin(pmin, from_part<L, K>(pmin_own));
-                n_nonexist += from_part<L, K>(nx_own);
-                fl |= from_part<L, K>(fl_own);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+            // charger c0 + j (past a ragged lane's range: its charger NC - 1 again, discarded)
+            const uint32_t v4 = row_of(j, nc, E), r4 = r4_of(j, E), v8 = 2u * v4, r8 = 2u * r4;
+            if (PK) {
+                w[j] = bld(rec_t, v4, r4);
+            } else {
+                w[j] = bld(s.word + plane, v4, r4);
+                aux[PK ? 0 : j] = bld(s.aux + plane, v8, r8);
+            }
+            run_[j] = bld(s.soc, v8, r8);
+            if (REQ) req[REQ ? j : 0] = bld(s.req + plane, v8, r8);
+        }
+    }
+    // Requested_SOC[c, t-1] of charger j of the lane; without the stream 1.0, or the cleared 0.0 of a replayed day
+    __device__ __forceinline__ double req_of(int j, const Params &p) const {
+        return REQ ? req[REQ ? j : 0] : (p.req_zero ? 0.0 : 1.0);
+    }
+
+    // the group's step; s_act holds its actions tile (committed), s_obs is the wavefront's observation tile
+    __device__ __forceinline__ void run(const float *s_act, float *s_obs, float *obs, double *reward, uint8_t *done,
+                                        int64_t E, int t, int vec_io, const StepConst &k, const Params &p,
+                                        const DeviceState &s, const InfoPtrs &info, int lane) {
+        const int Ad = p.act_dim, O = p.obs_dim;
+        const int le = lane / L, part = lane % L;
+        const bool leader = part == 0;
+        const int c0 = part * CPL;
+        const int nc = (NC - c0) < CPL ? NC - c0 : CPL;
+        const size_t plane = (size_t)t * NC * (size_t)E;
+        const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;
+        const float *a_row = s_act + le * Ad;
+        float *o_row = s_obs + le * O;
+        float av[CPL];
+        float amin = 0.0f;
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+            av[j] = a_row[(c0 + j) < NC ? c0 + j : NC - 1];
+            amin = __builtin_fminf(amin, av[j]);   // a NaN action is not negative (fmin drops it)
+        }
+        const float bess_action = p.bess ? a_row[NC] : 0.0f;
+        const int k_soc = p.pv ? 8 : 4;
+        if (live && leader) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, fpv, fpr);
+
+        double pen_v = 0.0, p_ch = 0.0, p_dis = 0.0;
+        uint32_t n_nonexist = 0, fl = 0;
+        if (__builtin_amdgcn_ballot_w64(live && amin < 0.0f) == 0) {
+            // the fast loop: no negative action in the wave, so no negative power (p_dis stays 0.0)
+            double seq_pos = 0.0, pmin = __builtin_inf();
+            int n_pos = 0;
+            double qv[L > 1 ? CPL : 1];
+            if (live) {
 #pragma unroll
                 for (int j = 0; j < CPL; ++j) {
-                    const double qk = from_part<L, K>(qv[L > 1 ? j : 0]);
-                    pen_v = leader ? pen_v + qk : pen_v;
+                    const int c = c0 + j;
+                    if (NC % L != 0 && j >= nc) {   // a ragged lane's range ends: adds nothing
+                        qv[L > 1 ? j : 0] = 0.0;
+                        continue;
+                    }
+                    const uint32_t capi = (w[j] >> W_CAP_SHIFT) & 0xffu;
+                    const bool occ = (w[j] & W_OCC) != 0;
+                    const ChargerResult r = charger_step<true, true>(p, PK ? (w[j] & ~W_STATIC) : w[j],
+                                                                     PK ? 0.0 : aux[PK ? 0 : j], run_[j], req_of(j, p), av[j],
+                                                                     t, recip_cap((double)capi));
+                    bst<kNT>(s.soc, 2u * row_of(j, nc, E), (PK && !occ) ? (double)rec_soc(w[j]) : r.soc,
+                             2u * r4_of(j, E));
+                    o_row[k_soc + c] = (float)r.soc;
+                    o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[j]);
+                    n_nonexist += r.nx;
+                    fl |= r.fl;
+                    if (L > 1) qv[L > 1 ? j : 0] = r.q;
+                    pen_v += r.q;
+                    const bool ip = r.pw > 0.0;
+                    seq_pos += __builtin_fmax(r.pw, 0.0);
+                    n_pos += ip ? 1 : 0;
+                    pmin = __builtin_fmin(pmin, ip ? r.pw : __builtin_inf());
+                    // chargers in order (groups of kWideSB): charger j waits only for its own loads
+                    if ((j + 1) % kWideSB == 0) __builtin_amdgcn_sched_barrier(0);
                 }
-            };
-            gather(std::integral_constant<int, 1>{});
-            if constexpr (L > 2) {
-                gather(std::integral_constant<int, 2>{});
-                gather(std::integral_constant<int, 3>{});
             }
-            split = with_pos > 1;
-        }
-        p_ch = seq_pos;
-        const bool pos_slow = live && leader && (n_pos >= 8 || split) && !(seq_pos <= pmin * 0x1.0p28);
-        if (__builtin_amdgcn_ballot_w64(pos_slow)) {   // wave-uniform: rare
-            if (pos_slow) {
-                // the compacted positive powers again, in charger order: an occupied charger charging with
-                // a > 0 under bounded charging bills pc (charger.py:58-94); nothing else is positive here
-                PairwiseSum pos;
-                pos.init();
+            // numpy sums fewer than 8 positive powers in order: one lane's running sum is that sum; two lanes'
+            // partial sums combined are that sum only when one of them is empty or the sum is exact
+            bool split = false;
+            if constexpr (L > 1) {
+                // the other lanes' totals (exact combinations), and their penalties after the first lane's own,
+                // in charger order (adding a +0.0 term is exact)
+                const double seq_own = seq_pos, pmin_own = pmin;
+                const int n_own = n_pos;
+                const uint32_t nx_own = n_nonexist, fl_own = fl;
+                int with_pos = n_own > 0 ? 1 : 0;
+                auto gather = [&](auto kc) {
+                    constexpr int K = decltype(kc)::value;
+                    const int nk = (int)from_part<L, K>((uint32_t)n_own);
+                    with_pos += nk > 0 ? 1 : 0;
+                    n_pos += nk;
+                    seq_pos += from_part<L, K>(seq_own);
+                    pmin = __builtin_fmin(pmin, from_part<L, K>(pmin_own));
+                    n_nonexist += from_part<L, K>(nx_own);
+                    fl |= from_part<L, K>(fl_own);
+#pragma unroll
+                    for (int j = 0; j < CPL; ++j) {
+                        const double qk = from_part<L, K>(qv[L > 1 ? j : 0]);
+                        pen_v = leader ? pen_v + qk : pen_v;
+                    }
+                };
+                gather(std::integral_constant<int, 1>{});
+                if constexpr (L > 2) {
+                    gather(std::integral_constant<int, 2>{});
+                    gather(std::integral_constant<int, 3>{});
+                }
+                split = with_pos > 1;
+            }
+            p_ch = seq_pos;
+            const bool pos_slow = live && leader && (n_pos >= 8 || split) && !(seq_pos <= pmin * 0x1.0p28);
+            if (__builtin_amdgcn_ballot_w64(pos_slow)) {   // wave-uniform: rare
+                if (pos_slow) {
+                    // the compacted positive powers again, in charger order: an occupied charger charging with
+                    // a > 0 under bounded charging bills pc (charger.py:58-94); nothing else is positive here
+                    PairwiseSum pos;
+                    pos.init();
+#pragma unroll 1
+                    for (int c = 0; c < NC; ++c) {
+                        const uint32_t wc = PK ? bld(rec_t, el4, (uint32_t)c * (uint32_t)E * 4u)
+                                               : bld(s.word + plane, el4, (uint32_t)c * (uint32_t)E * 4u);
+                        const float a = a_row[c];
+                        const double pc = charging_power(p, a);
+                        if ((wc & W_OCC) && p.bounded && a > 0.0f && pc > 0.0) pos.push(pc);
+                    }
+                    p_ch = pos.result();
+                }
+            }
+        } else {
+            // a wave with a discharging action: numpy's pairwise order for both signs (PairwiseSum), one
+            // charger at a time on the env's first lane, its inputs re-read from memory and the actions tile
+            PairwiseSum pos, neg;
+            pos.init();
+            neg.init();
+            if (live && leader) {
 #pragma unroll 1
                 for (int c = 0; c < NC; ++c) {
-                    const uint32_t wc = PK ? bld(rec_t, el4, (uint32_t)c * (uint32_t)E * 4u)
-                                           : bld(s.word + plane, el4, (uint32_t)c * (uint32_t)E * 4u);
-                    const float a = a_row[c];
-                    const double pc = charging_power(p, a);
-                    if ((wc & W_OCC) && p.bounded && a > 0.0f && pc > 0.0) pos.push(pc);
+                    const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
+                    const uint32_t wc = PK ? bld(rec_t, el4, r4) : bld(s.word + plane, el4, r4);
+                    const double auxc = PK ? 0.0 : bld(s.aux + plane, el8, r8);
+                    const double runc = bld(s.soc, el8, r8);
+                    const double reqc = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
+                    const uint32_t capi = (wc >> W_CAP_SHIFT) & 0xffu;
+                    const bool occ = (wc & W_OCC) != 0;
+                    const ChargerResult r = charger_step<true, true>(p, PK ? (wc & ~W_STATIC) : wc, auxc, runc, reqc,
+                                                                     a_row[c], t, recip_cap((double)capi));
+                    bst<kNT>(s.soc, el8, (PK && !occ) ? (double)rec_soc(wc) : r.soc, r8);
+                    o_row[k_soc + c] = (float)r.soc;
+                    o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : wc);
+                    n_nonexist += r.nx;
+                    fl |= r.fl;
+                    pen_v += r.q;
+                    if (r.pw > 0.0) pos.push(r.pw);
+                    if (r.pw < 0.0) neg.push(r.pw);
                 }
-                p_ch = pos.result();
             }
+            p_ch = pos.result();
+            p_dis = neg.result();
         }
-    } else {
-        // a wave with a discharging action: numpy's pairwise order for both signs (PairwiseSum), one
-        // charger at a time on the env's first lane, its inputs re-read from memory and the actions tile
-        PairwiseSum pos, neg;
-        pos.init();
-        neg.init();
         if (live && leader) {
-#pragma unroll 1
-            for (int c = 0; c < NC; ++c) {
-                const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
-                const uint32_t wc = PK ? bld(rec_t, el4, r4) : bld(s.word + plane, el4, r4);
-                const double auxc = PK ? 0.0 : bld(s.aux + plane, el8, r8);
-                const double runc = bld(s.soc, el8, r8);
-                const double reqc = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
-                const uint32_t capi = (wc >> W_CAP_SHIFT) & 0xffu;
-                const bool occ = (wc & W_OCC) != 0;
-                const ChargerResult r = charger_step<true, true>(p, PK ? (wc & ~W_STATIC) : wc, auxc, runc, reqc,
-                                                                 a_row[c], t, recip_cap((double)capi));
-                bst<kNT>(s.soc, el8, (PK && !occ) ? (double)rec_soc(wc) : r.soc, r8);
-                o_row[k_soc + c] = (float)r.soc;
-                o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : wc);
-                n_nonexist += r.nx;
-                fl |= r.fl;
-                pen_v += r.q;
-                if (r.pw > 0.0) pos.push(r.pw);
-                if (r.pw < 0.0) neg.push(r.pw);
-            }
+            pen_v += (t == 0) ? pen0_l : 0.0;   // python index -1 slot; every per-charger term is 0 at t = 0
+            env_tail<false>(p, s, info, e0, (uint32_t)le, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action,
+                            p_ch, p_dis, pen_v, 100.0 * (double)n_nonexist, fl, o_row, k.v, fpv, fpr,
+                            info.episode_return ? ret_l : 0.0, 0.0, reward, done);
         }
-        p_ch = pos.result();
-        p_dis = neg.result();
+        wave_lds_fence();
+        copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
     }
-    if (live && leader) {
-        pen_v += (t == 0) ? pen0_l : 0.0;   // python index -1 slot; every per-charger term is 0 at t = 0
-        env_tail<false>(p, s, info, e0, (uint32_t)le, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action, p_ch,
-                        p_dis, pen_v, 100.0 * (double)n_nonexist, fl, o_row, k.v, fpv, fpr,
-                        info.episode_return ? ret_l : 0.0, 0.0, reward, done);
-    }
+};
+
+// Groups of envs per wavefront of the wide kernel (G): the headline's N = 10 steps two groups of 32 envs per
+// wavefront (1,024 wavefronts at 65,536 envs, one per SIMD), so one group's arithmetic and stores overlap
+// the other's loads; config 5's N = 50 keeps one group (its registers are full at two waves per SIMD).
+#ifndef SNG_WIDE_G10
+#define SNG_WIDE_G10 2
+#endif
+__host__ __device__ constexpr int wide_groups(int NC) { return NC == 10 ? SNG_WIDE_G10 : 1; }
+__host__ __device__ constexpr int wide_waves(int L, int G) {
+    return (L / G) < 1 ? 1 : ((L / G) < SNG_WIDE_WPE ? L / G : SNG_WIDE_WPE);
+}
+
+// L lanes per env (1, 2 or 4): lane `part` of an env steps chargers [part * CPL, min(NC, (part + 1) * CPL)),
+// CPL = ceil(NC / L).  The env's lanes are adjacent (one DPP quad); the partial charging sums, counts and
+// minima combine exactly on the first lane (a sum the exactness test accepts is exact in any order, and
+// fewer than 8 powers are numpy's in-order sum when one lane holds them all), the first lane adds the
+// other lanes' vehicle penalties after its own in charger order (Python's sum, penaliser.py:55), and the
+// rare exact-order paths run on the first lane over all chargers.  G groups of 64 / L envs per wavefront.
+// Waves per SIMD the register budget is sized for: L / G (every wave of the E = 65,536 grid resident at
+// once); SNG_WIDE_WPE (A/B builds) caps it.  Config 5 with four lanes per env and a 3-wave budget (166
+// VGPRs, no spills, 3 of the 4,096 waves per SIMD resident): 29.6-29.8 us against 23.4 us with two lanes
+// (profiles/r03_ab_config5_four_lanes.txt).
+template <int NC, int L, int G, bool PK, bool REQ, bool NOISE>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(wide_waves(L, G), wide_waves(L, G)))) void
+step_wide_kernel(const float *__restrict__ act, float *__restrict__ obs, double *__restrict__ reward,
+                 uint8_t *__restrict__ done, int64_t E, int t, int vec_io, StepConst k, Params p, DeviceState s,
+                 InfoPtrs info) {
+    static_assert(L == 1 || L == 2 || L == 4, "one, two or four lanes per env");
+    static_assert(G == 1 || G == 2, "one or two groups per wavefront");
+    using Grp = WideGroup<NC, L, PK, REQ, NOISE>;
+    using Lay = WideLds<NC, L>;
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    const int lane = threadIdx.x;
+    float *s_obs = lds + G * Lay::ACT;   // [G] actions tiles, then the observation tile the groups share
+    // the groups as named objects, not an array (an array of them kept config 5's registers from being
+    // promoted: 188 VGPRs spilled at N = 50)
+    Grp g0, g1;
+    const int64_t e0 = (int64_t)blockIdx.x * G * Grp::WENVS;   // the grid covers E: the first group has an env
+    const bool second = G == 2 && e0 + Grp::WENVS < E;         // a second group past E (odd tail) is skipped
+    g0.issue(e0, act, E, t, vec_io, p, s, info, lane);
+    if constexpr (G == 2) g1.issue(second ? e0 + Grp::WENVS : e0, act, E, t, vec_io, p, s, info, lane);
+    g0.act_tile.commit(lds, lane);
+    if constexpr (G == 2) g1.act_tile.commit(lds + Lay::ACT, lane);
     wave_lds_fence();
-    copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
+    g0.run(lds, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
+    if constexpr (G == 2) {
+        if (second) {
+            wave_lds_fence();   // the first group's copy-out reads precede the second group's tile writes
+            g1.run(lds + Lay::ACT, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
+        }
+    }
     if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_fetch_add(s.episode, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -2031,21 +2111,22 @@ template <int NC>
 static void launch_wide(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
                         const float *act, float *obs, double *reward, uint8_t *done, int64_t E, int t, int vec_io,
                         hipStream_t stream, const LaunchEvents *ev) {
-    constexpr int L = wide_lanes(NC);
+    constexpr int L = wide_lanes(NC), G = wide_groups(NC);
     StepConst k;
     for (int i = 0; i < CST_COUNT; ++i) k.v[i] = step_constant(&tab, t, i);
     const bool req = p.req_stream && !p.req_zero;
     const int v = (p.packed ? 4 : 0) | (req ? 2 : 0) | (p.noise ? 1 : 0);
     void (*kerns[8])(const float *, float *, double *, uint8_t *, int64_t, int, int, StepConst, Params, DeviceState,
                      InfoPtrs) = {
-        step_wide_kernel<NC, L, false, false, false>, step_wide_kernel<NC, L, false, false, true>,
-        step_wide_kernel<NC, L, false, true, false>,  step_wide_kernel<NC, L, false, true, true>,
-        step_wide_kernel<NC, L, true, false, false>,  step_wide_kernel<NC, L, true, false, true>,
-        step_wide_kernel<NC, L, true, true, false>,   step_wide_kernel<NC, L, true, true, true>};
+        step_wide_kernel<NC, L, G, false, false, false>, step_wide_kernel<NC, L, G, false, false, true>,
+        step_wide_kernel<NC, L, G, false, true, false>,  step_wide_kernel<NC, L, G, false, true, true>,
+        step_wide_kernel<NC, L, G, true, false, false>,  step_wide_kernel<NC, L, G, true, false, true>,
+        step_wide_kernel<NC, L, G, true, true, false>,   step_wide_kernel<NC, L, G, true, true, true>};
     auto kern = kerns[v];
-    constexpr int WENVS = WideLds<NC, L>::WENVS;
-    const dim3 grid((unsigned)((E + WENVS - 1) / WENVS)), block(kWave);
-    const uint32_t lds = (uint32_t)WideLds<NC, L>::BYTES;
+    using Lay = WideLds<NC, L>;
+    constexpr int ENVS = Lay::WENVS * G;   // envs per wavefront
+    const dim3 grid((unsigned)((E + ENVS - 1) / ENVS)), block(kWave);
+    const uint32_t lds = (uint32_t)((size_t)(G * Lay::ACT + Lay::OBS) * 4);
     if (ev)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,
                               vec_io, k, p, s, info);
@@ -2162,8 +2243,8 @@ int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) 
         return snprintf(buf, (size_t)len, "void sng::step_lean_kernel<%d, %s, %s>", p.n, p.packed ? "true" : "false",
                         (p.req_stream && !p.req_zero) ? "true" : "false");
     if (wide_step(p, info_diag(info)))
-        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %d, %s, %s, %s>", p.n, wide_lanes(p.n),
-                        p.packed ? "true" : "false", (p.req_stream && !p.req_zero) ? "true" : "false",
+        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %d, %d, %s, %s, %s>", p.n, wide_lanes(p.n),
+                        wide_groups(p.n), p.packed ? "true" : "false", (p.req_stream && !p.req_zero) ? "true" : "false",
                         p.noise ? "true" : "false");
 #endif
     int nc = 0, lanes = 1;

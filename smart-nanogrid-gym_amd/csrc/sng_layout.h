@@ -181,6 +181,7 @@ struct InfoPtrs {
     uint32_t *flags;
     double *episode_return;
     double *charger_power, *vehicle_soc;   // [E][N], DIAG only
+    uint32_t *flag_any;                    // SngInfo.flag_summary: OR of every raised flag (rare atomics)
 };
 
 }  // namespace sng

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SNG_LIBRARY", os.path.join(os.path.dirname(PKG_DIR), 
 DATA_DIR = os.path.join(PKG_DIR, "data")
 IRRADIANCE_FILE = os.path.join(DATA_DIR, "solar_irradiance_1min.f64")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 SNG_OK = 0
 RNG_REFERENCE = 0
 RNG_DEVICE = 1
@@ -86,7 +86,8 @@ class SngInfo(ctypes.Structure):
     _fields_ = [(f, ctypes.c_void_p) for f in INFO_FIELDS] + [("flags", ctypes.c_void_p),
                                                                ("episode_return", ctypes.c_void_p),
                                                                ("charger_power", ctypes.c_void_p),
-                                                               ("vehicle_soc", ctypes.c_void_p)]
+                                                               ("vehicle_soc", ctypes.c_void_p),
+                                                               ("flag_summary", ctypes.c_void_p)]
 
 
 class SngScenario(ctypes.Structure):

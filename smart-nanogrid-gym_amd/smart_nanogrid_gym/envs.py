@@ -70,13 +70,12 @@ class SmartNanogridEnv(_Base):
         v._act_h.numpy()[0] = np.asarray(actions, dtype=np.float32).reshape(-1)
         with torch.cuda.device(v.device):
             v.actions_d.copy_(v._act_h, non_blocking=True)
-            obs_d, rew_d, done_d = v.step_tensors(v.actions_d)
-            v._obs_h.copy_(obs_d, non_blocking=True)
-            v._rew_h.copy_(rew_d, non_blocking=True)
-            v._done_h.copy_(done_d, non_blocking=True)
-            v._flags_h.copy_(v.flags_d, non_blocking=True)
+            v.step_tensors(v.actions_d)
+            v._out_h.copy_(v._out_d, non_blocking=True)   # reward, obs, done, flag summary
             torch.cuda.current_stream(v.device).synchronize()
-        v._raise_flags(v._flags_h.numpy())
+        flags = v._step_flags()
+        if flags is not None:
+            v._raise_flags(flags)
         terminated = bool(v._done_h.numpy()[0])
         self.timestep = 0 if terminated else self.timestep + 1
         self.simulated_single_day = terminated

@@ -191,7 +191,7 @@ def evaluate_models(models, episodes=100, *, seed=0, device=0, rng="reference", 
                 actions[sl] = _policy_actions(models[name], obs[sl])
             obs, rew, _ = venv.step_tensors(actions)
             totals += rew
-        venv._raise_flags(venv.flags_d.cpu().numpy())   # the reference's errors, as step() raises them
+        venv.check_errors()   # the reference's errors of any step of the day, as step() raises them
         totals = totals.cpu().numpy().reshape(M, episodes)
     finally:
         venv.close()

@@ -85,11 +85,24 @@ class DayReturnExchange:
             self.work[k] = None
         return self.snap[k]
 
-    def gather(self, k):
-        """Start the all-gather of buffer k (after the replay that fills it has been launched)."""
+    def gather(self, k, stream=None):
+        """Start the all-gather of buffer k (after the replay that fills it has been launched).  stream: the
+        stream that replay was launched on (a torch.cuda.Stream or a raw hipStream_t handle, as given to
+        EpisodeGraph.launch), when it is not the current stream: the current stream then waits for it, so
+        the copy or collective below cannot read a half-filled snapshot."""
+        on_gpu = self.snap[k].is_cuda
+        cur = torch.cuda.current_stream(self.snap[k].device) if on_gpu else None
+        if stream is not None and on_gpu:
+            if not isinstance(stream, torch.cuda.Stream):
+                stream = torch.cuda.ExternalStream(int(stream), device=self.snap[k].device)
+            if stream != cur:
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                cur.wait_event(ev)
         if self.host:
             self.staged[k].copy_(self.snap[k], non_blocking=True)
-            torch.cuda.current_stream(self.snap[k].device).synchronize()
+            if on_gpu:
+                cur.synchronize()
             self.work[k] = dist.all_gather(list(self.out[k].unbind(0)), self.staged[k], group=self.group,
                                            async_op=True)
         elif self.fused:

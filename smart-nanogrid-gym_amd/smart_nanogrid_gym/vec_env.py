@@ -21,6 +21,7 @@ Reference behaviour mirrored per env (smart_nanogrid_gym/envs/smart_nanogrid_env
   errors   -> the reference's ValueErrors, raised after the step that hit them
 """
 import ctypes
+import time
 import warnings
 
 import numpy as np
@@ -72,6 +73,10 @@ class SmartNanogridVecEnv(_VecEnvBase):
         self.device = torch.device("cuda", device)
         self.rng_mode = _native.RNG_DEVICE if rng == "device" else _native.RNG_REFERENCE
         self._seed = int(seed)
+        if self._seed < 0 or (self.rng_mode == _native.RNG_REFERENCE
+                              and self._seed + int(env_offset) + int(num_envs) > 2 ** 32):
+            raise ValueError(f"seed {self._seed}: reference-RNG env i is seeded seed + env_offset + i, which must "
+                             "stay in numpy's [0, 2**32)")
         cfg = self.settings.to_native()
         h = ctypes.c_void_p()
         check(lib().sng_create(ctypes.byref(cfg), device, self.num_envs, self._seed, ctypes.byref(h)))
@@ -84,36 +89,46 @@ class SmartNanogridVecEnv(_VecEnvBase):
         self.obs_dim, self.act_dim, self.timesteps = dims.obs_dim, dims.act_dim, dims.timesteps
         self.step_lanes = dims.step_lanes_per_env
         self.slots = dims.slots
-        E = self.num_envs
+        E, O = self.num_envs, self.obs_dim
         dev = self.device
         self.actions_d = torch.zeros((E, self.act_dim), dtype=torch.float32, device=dev)
-        self.obs_d = torch.zeros((E, self.obs_dim), dtype=torch.float32, device=dev)
-        self.reward_d = torch.zeros(E, dtype=torch.float64, device=dev)
-        self.done_d = torch.zeros(E, dtype=torch.uint8, device=dev)
-        self.flags_d = torch.zeros(E, dtype=torch.int32, device=dev)
+        # What the numpy (SB3) path brings back after every step, as one device block with one pinned host
+        # mirror, so a step costs one device-to-host copy: reward f64 [E] | obs f32 [E][O] | done u8 [E] |
+        # the flag summary word (SngInfo.flag_summary), sections 256 B aligned.
+        al = lambda x: (x + 255) // 256 * 256   # noqa: E731
+        o_obs = al(E * 8)
+        o_done = al(o_obs + E * O * 4)
+        o_flag = al(o_done + E)
+        self._out_d = torch.zeros(o_flag + 256, dtype=torch.uint8, device=dev)
+        self._out_h = torch.zeros(o_flag + 256, dtype=torch.uint8, pin_memory=True)
+
+        def views(buf):
+            return (buf[:E * 8].view(torch.float64), buf[o_obs:o_obs + E * O * 4].view(torch.float32).view(E, O),
+                    buf[o_done:o_done + E], buf[o_flag:o_flag + 4].view(torch.int32))
+        self.reward_d, self.obs_d, self.done_d, self.flag_summary_d = views(self._out_d)
+        self._rew_h, self._obs_h, self._done_h, self._flag_summary_h = views(self._out_h)
+        self.flags_d = torch.zeros(E, dtype=torch.int32, device=dev)   # per-step flags, with info=True
         self.return_d = torch.zeros(E, dtype=torch.float64, device=dev)
         self.info_d = {}
         self.charger_power_d = self.vehicle_soc_d = None
         self._recorders = []
         self._info = _native.SngInfo()
-        self._info.flags = self.flags_d.data_ptr()
+        # errors are watched through the summary word (touched only when an env raises a flag), so the
+        # step stores no per-env flags; info=True adds the per-step per-env flags to the diagnostics
+        self._info.flag_summary = self.flag_summary_d.data_ptr()
         self._info.episode_return = self.return_d.data_ptr()
         if info:
             self._enable_info()
-        # pinned host mirrors for the numpy (SB3) path
-        pin = dict(pin_memory=True)
-        self._act_h = torch.zeros((E, self.act_dim), dtype=torch.float32, **pin)
-        self._obs_h = torch.zeros((E, self.obs_dim), dtype=torch.float32, **pin)
-        self._rew_h = torch.zeros(E, dtype=torch.float64, **pin)
-        self._done_h = torch.zeros(E, dtype=torch.uint8, **pin)
-        self._flags_h = torch.zeros(E, dtype=torch.int32, **pin)
+        # pinned host mirror of the actions for the numpy (SB3) path
+        self._act_h = torch.zeros((E, self.act_dim), dtype=torch.float32, pin_memory=True)
+        self._prof = None
         self._pending = None
         self._warned_breakpoint = False
         self._last_reset = None   # 'generated', 'replay' or 'injected': how the loaded day began
         self.closed = False
         # SB3 2.x VecEnv state: the reset infos (the reference's reset returns {}, :351), and the seeds /
         # options that seed() / set_options() leave for the next reset
-        self.reset_infos = [{} for _ in range(E)]
+        self.reset_infos = None
         self._seeds = [None] * E
         self._options = [{} for _ in range(E)]
         if _VecEnvBase is not object:   # pragma: no cover - SB3 is not in the image
@@ -142,6 +157,7 @@ class SmartNanogridVecEnv(_VecEnvBase):
             self.info_d = {f: torch.zeros(E, dtype=torch.float64, device=dev) for f in _native.INFO_FIELDS}
             for f, t in self.info_d.items():
                 setattr(self._info, f, t.data_ptr())
+            self._info.flags = self.flags_d.data_ptr()
         if per_charger and self.charger_power_d is None:
             self.charger_power_d = torch.zeros((E, N), dtype=torch.float64, device=dev)
             self.vehicle_soc_d = torch.zeros((E, N), dtype=torch.float64, device=dev)
@@ -309,7 +325,7 @@ class SmartNanogridVecEnv(_VecEnvBase):
             algorithm_used = o.pop("algorithm_used", algorithm_used)
             environment_mode = o.pop("environment_mode", environment_mode)
             kwargs = {**o, **kwargs}
-        self.reset_infos = [{} for _ in range(self.num_envs)]
+        self.reset_infos = None   # the reference's reset returns {} per env (:351): made on first access
         if algorithm_used:
             self.settings.algorithm_used = algorithm_used
         if environment_mode:
@@ -330,37 +346,95 @@ class SmartNanogridVecEnv(_VecEnvBase):
         actions = self._pending
         self._pending = None
         E = self.num_envs
+        prof = self._prof
+        t0 = time.perf_counter() if prof is not None else 0.0
         a = np.asarray(actions, dtype=np.float32).reshape(E, self.act_dim)
         self._act_h.numpy()[...] = a
+        if prof is not None:
+            ta = time.perf_counter()
         stream = torch.cuda.current_stream(self.device)
         with torch.cuda.device(self.device):
+            if prof is not None:
+                ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+                ev[0].record(stream)
             self.actions_d.copy_(self._act_h, non_blocking=True)
+            if prof is not None:
+                ev[1].record(stream)
             self.step_tensors(self.actions_d)
-            self._obs_h.copy_(self.obs_d, non_blocking=True)
-            self._rew_h.copy_(self.reward_d, non_blocking=True)
-            self._done_h.copy_(self.done_d, non_blocking=True)
-            self._flags_h.copy_(self.flags_d, non_blocking=True)
+            if prof is not None:
+                ev[2].record(stream)
+            self._out_h.copy_(self._out_d, non_blocking=True)   # reward, obs, done, flag summary: one copy
+            if prof is not None:
+                ev[3].record(stream)
+                t1 = time.perf_counter()
+            # the per-env info dicts SB3 expects (one fresh dict per env) are built while the device works
+            last = lib().sng_get_timestep(self._h) + 1 >= self.timesteps
+            infos = None if last else [{} for _ in range(E)]
             stream.synchronize()
-        self._raise_flags(self._flags_h.numpy())
+        if prof is not None:
+            t2 = time.perf_counter()
+        flags = self._step_flags()
         obs = self._obs_h.numpy().copy()
         rewards = self._rew_h.numpy().copy()
         dones = self._done_h.numpy().astype(bool)
-        infos = [{} for _ in range(E)]
-        flags = self._flags_h.numpy()
-        if flags.any():
-            for i in np.nonzero(flags & _native.FLAG_V2X_BREAKPOINT)[0]:
-                infos[i]["v2x_breakpoint"] = True
+        if flags is not None:
+            self._raise_flags(flags)
         if dones.any():
-            for i in range(E):
-                infos[i]["terminal_observation"] = obs[i]
-                infos[i]["TimeLimit.truncated"] = False
             # DummyVecEnv's automatic reset: a new day; seeds and options left by seed() / set_options()
             # wait for the caller's next reset()
+            infos = [{"terminal_observation": o, "TimeLimit.truncated": False} for o in obs]
+        elif infos is None:
+            infos = [{} for _ in range(E)]
+        if flags is not None:
+            for i in np.nonzero(flags & _native.FLAG_V2X_BREAKPOINT)[0]:
+                infos[i]["v2x_breakpoint"] = True
+        if prof is not None:
+            t3 = time.perf_counter()
+            for k, x in (("actions_in", ta - t0), ("enqueue", t1 - ta), ("sync", t2 - t1), ("host_out", t3 - t2)):
+                prof.setdefault(k, []).append(x)
+            for k, (x, y) in (("h2d", (0, 1)), ("step", (1, 2)), ("d2h", (2, 3))):
+                prof.setdefault(k, []).append(ev[x].elapsed_time(ev[y]) * 1e-3)
+        if dones.any():
             self._check_mode()
             self._new_day()
-            self.reset_infos = [{} for _ in range(E)]
+            self.reset_infos = None   # made on first access
             obs = self._obs_to_host()
+            if prof is not None:
+                prof.setdefault("reset", []).append(time.perf_counter() - t3)
         return obs, rewards, dones, infos
+
+    def _step_flags(self):
+        """After a step's outputs reached the host: None when no env raised a flag since the last check
+        (the summary word, copied with the outputs, is 0), else the per-env SNG_FLAG_* raised since then
+        (the sticky flags, read and cleared; the summary is zeroed)."""
+        if int(self._flag_summary_h.numpy()[0]) == 0:
+            return None
+        return self._read_and_clear_flags()
+
+    def _read_and_clear_flags(self):
+        flags = np.zeros(self.num_envs, np.uint32)
+        with torch.cuda.device(self.device):
+            self.flag_summary_d.zero_()
+            check(lib().sng_read_errors(self._h, flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 1,
+                                        _stream_handle(self.device)), self._h)
+        self._flag_summary_h.zero_()
+        return flags.view(np.int32)
+
+    def check_errors(self):
+        """Raise the reference's exception for any flag an env raised since the last check (the device
+        path, step_tensors, raises nothing by itself); synchronises the current stream."""
+        with torch.cuda.device(self.device):
+            self._flag_summary_h.copy_(self.flag_summary_d)
+        flags = self._step_flags()
+        if flags is not None:
+            self._raise_flags(flags)
+
+    def profile_phases(self, on=True):
+        """Time the phases of every numpy step() (tools/sb3_path_bench.py): on=True starts recording,
+        on=False stops and returns {phase: [seconds per step]}."""
+        out = self._prof
+        self._prof = {} if on else None
+        return out
 
     def step(self, actions):
         self.step_async(actions)
@@ -372,9 +446,13 @@ class SmartNanogridVecEnv(_VecEnvBase):
         that seed from its first day).  seed=None picks a fresh seed.  Returns the per-env seeds.  The
         reference's own seed() is a no-op (smart_nanogrid_environment.py:362-365) and it seeds through the
         global RNGs instead."""
+        top = 2 ** 32 - self.num_envs - self.env_offset   # np.random.seed takes [0, 2^32): seed + offset + i too
         if seed is None:
-            seed = int(np.random.randint(0, np.iinfo(np.uint32).max, dtype=np.uint32))
+            seed = int(np.random.randint(0, max(top, 0) + 1, dtype=np.int64))
         seed = int(seed)
+        if seed < 0 or (self.rng_mode == _native.RNG_REFERENCE and seed > top):
+            raise ValueError(f"seed {seed}: reference-RNG env i is seeded seed + env_offset + i, which must stay "
+                             f"in numpy's [0, 2**32); use a seed in [0, {top}]")
         self._seeds = [seed + i for i in range(self.num_envs)]
         return list(self._seeds)
 
@@ -400,6 +478,17 @@ class SmartNanogridVecEnv(_VecEnvBase):
 
     def render(self, mode="human"):
         return None
+
+    @property
+    def reset_infos(self):
+        """SB3 2.x: the info dict of every env's last reset ({} per env, as the reference's reset returns)."""
+        if self._reset_infos is None:
+            self._reset_infos = [{} for _ in range(self.num_envs)]
+        return self._reset_infos
+
+    @reset_infos.setter
+    def reset_infos(self, value):
+        self._reset_infos = value
 
     # Per-env attributes get_attr / set_attr resolve env by env (the rest are shared by the batch: the
     # reference's constructor keywords, settings, spaces, the timestep).
@@ -499,7 +588,13 @@ class SmartNanogridVecEnv(_VecEnvBase):
         """Per-step diagnostics of the last step (numpy, names of the reference results dict)."""
         torch.cuda.current_stream(self.device).synchronize()
         out = {k: v.cpu().numpy() for k, v in self.info_d.items()}
-        out["flags"] = self.flags_d.cpu().numpy()
+        if self.info_d:   # the last step's per-env flags (written with the diagnostics)
+            out["flags"] = self.flags_d.cpu().numpy()
+        else:             # the sticky flags raised since the last check (not cleared here)
+            flags = np.zeros(self.num_envs, np.uint32)
+            check(lib().sng_read_errors(self._h, flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 0,
+                                        _stream_handle(self.device)), self._h)
+            out["flags"] = flags.view(np.int32)
         out["episode_return"] = self.return_d.cpu().numpy()
         return out
 
@@ -558,6 +653,10 @@ class SmartNanogridVecEnv(_VecEnvBase):
                                       ctypes.c_void_p(self.return_d.data_ptr()), _stream_handle(self.device)),
                   self._h)
         self._seed = None
+        # the blob carries its own seed and streams: a seed() or set_options() left for the next reset
+        # before the restore would re-seed the restored streams and reset the day counter there
+        self._seeds = [None] * self.num_envs
+        self._options = [{} for _ in range(self.num_envs)]
 
     # ------------------------------------------------------------------ the loaded day
     def get_scenarios(self, first=0, count=None, max_vehicles=8):
@@ -594,7 +693,9 @@ class SmartNanogridVecEnv(_VecEnvBase):
 
     def run_eager_days(self, actions, days=1):
         """`days` device-RNG days (reset + T steps each) launched eagerly from C, back to back, without
-        per-dispatch events (sng_time_step_kernels with ms = NULL); synchronises."""
+        per-dispatch events (sng_time_step_kernels with ms = NULL); synchronises.  A seed left by seed()
+        takes effect here (these days begin with resets)."""
+        self._apply_pending_seed()
         a = actions.contiguous()
         with torch.cuda.device(self.device):
             check(lib().sng_time_step_kernels(self._h, ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(self.obs_d.data_ptr()),
@@ -605,7 +706,9 @@ class SmartNanogridVecEnv(_VecEnvBase):
     def time_step_kernels(self, actions, days=1, with_resets=False):
         """Device time (ms) of every step kernel over `days` eager device-RNG days, from HIP
         start/stop events attached to each kernel dispatch; actions [T, E, act_dim] on the device.
-        with_resets: also return every day's reset time (ms), as (steps, resets)."""
+        with_resets: also return every day's reset time (ms), as (steps, resets).  A seed left by seed() takes
+        effect here (these days begin with resets)."""
+        self._apply_pending_seed()
         a = actions.contiguous()
         out = np.zeros(days * self.timesteps, np.float32)
         res = np.zeros(days, np.float32) if with_resets else None
@@ -640,7 +743,13 @@ class EpisodeGraph:
     def __init__(self, venv, actions, with_reset=True, days=1, day_returns=None):
         """days > 1 captures that many consecutive days (each with its reset) in one graph,
         which amortises the graph launch.  day_returns: optional device tensor [days, E] f64;
-        day d's returns accumulate into row d (instead of venv.return_d)."""
+        day d's returns accumulate into row d (instead of venv.return_d).  A seed left by seed() takes effect
+        here for a graph of whole days (with_reset); a steps-only graph steps the loaded day, so it is refused
+        while a seed waits for the next reset."""
+        if with_reset:
+            venv._apply_pending_seed()
+        elif venv._seeds[0] is not None:
+            raise ValueError("seed() waits for the next reset: reset before capturing a steps-only graph")
         self.venv = venv
         self.days = int(days)
         self.actions = actions.contiguous()

@@ -261,3 +261,103 @@ def test_failed_injection_invalidates_the_day():
     v.reset_tensors()
     v.step_tensors(torch.zeros((E, 11), device="cuda:0"))
     v.close()
+
+
+def test_pending_seed_applies_to_graph_and_eager_days():
+    """seed() left for the next reset applies at an EpisodeGraph of whole days (and run_eager_days /
+    time_step_kernels), which begin with resets: the graph's day is a fresh population's first day of that
+    seed.  A steps-only graph steps the loaded day, so it refuses while a seed waits."""
+    E, N = 512, 10
+    acts = torch.rand((24, E, N + 1), device="cuda:0")
+    v = SmartNanogridVecEnv(E, seed=4, rng="device", **KW)
+    v.reset_tensors()
+    for t in range(24):
+        v.step_tensors(acts[t])
+    v.seed(5)
+    with pytest.raises(ValueError, match="steps-only"):
+        EpisodeGraph(v, acts, with_reset=False)
+    g = EpisodeGraph(v, acts, with_reset=True)      # the seed applies here
+    bess0 = v.battery_state_of_charge()
+    g.launch()
+    fresh = SmartNanogridVecEnv(E, seed=5, rng="device", **KW)
+    fresh.set_battery_state_of_charge(bess0)
+    fresh.reset_tensors()
+    for t in range(24):
+        fresh.step_tensors(acts[t])
+    torch.testing.assert_close(v.return_d, fresh.return_d, rtol=0, atol=0)
+    # and an eager day started by time_step_kernels after another seed()
+    v.seed(6)
+    v.time_step_kernels(acts, days=1)
+    f6 = SmartNanogridVecEnv(E, seed=6, rng="device", **KW)
+    f6.set_battery_state_of_charge(fresh.battery_state_of_charge())
+    f6.reset_tensors()
+    for t in range(24):
+        f6.step_tensors(acts[t])
+    torch.testing.assert_close(v.return_d, f6.return_d, rtol=0, atol=0)
+    for x in (g, v, fresh, f6):
+        x.close()
+
+
+@pytest.mark.parametrize("rng", ["reference", "device"])
+def test_load_state_discards_a_pending_seed(rng):
+    """seed(s); load_state(blob); reset() continues the checkpoint's streams (its seed, RNG state
+    and day counter) instead of re-seeding them at the reset."""
+    E = 256
+    a = SmartNanogridVecEnv(E, seed=21, rng=rng, **KW)
+    a.reset_tensors()
+    for t in range(24):
+        a.step_tensors(torch.rand((E, 11), device="cuda:0"))
+    blob = a.save_state()
+    b = SmartNanogridVecEnv(E, seed=3, rng=rng, **KW)
+    b.load_state(blob)
+    a.seed(99)
+    a.load_state(blob)
+    oa, ob = a.reset_tensors().clone(), b.reset_tensors().clone()
+    assert torch.equal(oa, ob)
+    assert a.get_scenarios()[0] == b.get_scenarios()[0]
+    a.close()
+    b.close()
+
+
+def test_flag_summary_reports_errors_and_v2x_breakpoints():
+    """The numpy step() path watches the one-word flag summary (SngInfo.flag_summary) instead of a per-env
+    flag store: a V2X station whose demand goes negative marks exactly the envs that hit the reference's
+    breakpoint() (central_management_system.py:160-165) in infos, step after step, and a negative action on
+    a non-V2X station raises the reference's ValueError (:158-159); the device path raises it at
+    check_errors()."""
+    E = 64
+    v2x = dict(KW, vehicle_to_everything=True)
+    v = SmartNanogridVecEnv(E, seed=2, rng="device", info=True, **v2x)   # per-env flags in the diagnostics too
+    q = SmartNanogridVecEnv(E, seed=2, rng="device", **v2x)              # the default: summary word only
+    v.reset()
+    q.reset()
+    rng = np.random.default_rng(1)
+    seen = 0
+    for t in range(24):
+        a = np.zeros((E, 11), np.float32)
+        a[:, :10] = -rng.random((E, 10))                  # everything discharges
+        _, rv, _, iv = v.step(a)
+        _, rq, _, iq = q.step(a)
+        np.testing.assert_array_equal(rv, rq)
+        flagged = v.last_info()["flags"] & _native.FLAG_V2X_BREAKPOINT
+        got = np.array(["v2x_breakpoint" in d for d in iq])
+        np.testing.assert_array_equal(got, flagged != 0)
+        np.testing.assert_array_equal(got, np.array(["v2x_breakpoint" in d for d in iv]))
+        seen += int(got.sum())
+    assert seen > 0
+    v.close()
+    q.close()
+    n = SmartNanogridVecEnv(E, seed=2, rng="device", **KW)
+    n.reset()
+    bad = np.zeros((E, 11), np.float32)
+    with pytest.raises(ValueError, match="power_demand"):
+        for t in range(24):
+            bad[:, :10] = -1.0
+            n.step(bad)
+    n.reset_tensors()
+    n.step_tensors(torch.from_numpy(bad).to(n.device))
+    with pytest.raises(ValueError, match="power_demand"):
+        n.check_errors()
+    n.step_tensors(torch.zeros((E, 11), device=n.device))
+    n.check_errors()   # cleared by the raise above: a clean step raises nothing
+    n.close()

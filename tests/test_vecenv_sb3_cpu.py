@@ -36,6 +36,8 @@ def test_with_sb3_the_class_is_an_sb3_vecenv():
 def _bare(cls, n):
     v = cls.__new__(cls)
     v.num_envs = n
+    v.env_offset = 0
+    v.rng_mode = 0   # _native.RNG_REFERENCE
     v._seeds = [None] * n
     v._options = [{} for _ in range(n)]
     return v
@@ -51,7 +53,18 @@ def test_seed_and_options_wait_for_the_next_reset(with_sb3):
     assert v.seed(11) == [11, 12, 13, 14]
     assert v._seeds == [11, 12, 13, 14]
     s = v.seed()
-    assert s == [s[0] + i for i in range(4)] and 0 <= s[0] < 2 ** 32
+    assert s == [s[0] + i for i in range(4)] and 0 <= s[0] and s[-1] < 2 ** 32
+    # reference-RNG env i is np.random.seed(seed + env_offset + i), numpy's range is [0, 2^32)
+    assert v.seed(2 ** 32 - 4)[-1] == 2 ** 32 - 1
+    for bad in (2 ** 32 - 3, -1):
+        with pytest.raises(ValueError, match="2\\*\\*32"):
+            v.seed(bad)
+    v.env_offset = 1000
+    with pytest.raises(ValueError):
+        v.seed(2 ** 32 - 1000)
+    for _ in range(200):   # a fresh seed keeps every env's seed in range
+        assert v.seed()[-1] + v.env_offset < 2 ** 32
+    v.env_offset = 0
     v.set_options({"generate_new_initial_values": False})
     assert v._options == [{"generate_new_initial_values": False}] * 4
     v.set_options()
