@@ -42,6 +42,9 @@ for s in $STEPS; do
     memfloor) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_memfloor.so run memfloor 300 python bench.py --no-cpu-baseline
            SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_memfloor.so run memfloor_cfg5 300 python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 ;;
     reset) run reset_bench 600 python tools/reset_bench.py ;;
+    layout) run stepmem2 300 tools/stepmem2 ;;
+    sb3)   run sb3_path 600 python tools/sb3_path_bench.py
+           run sb3_path_device 600 python tools/sb3_path_bench.py --rng device ;;
     pmc5)  run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc5_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 2 --warmup 1 --graph-days 1 --timing-days 1
            run pmc5_write 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/pmc5_write -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 2 --warmup 1 --graph-days 1 --timing-days 1 ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1

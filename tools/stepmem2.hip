@@ -518,7 +518,15 @@ int main() {
             bytes);
         run_copy<12, 14>("copy 1024 waves 12+14 KiB", cin, cout, 1024);
         run<2, 1, true>("soa L2 packed env", B, E, bytes);
+        run<2, 2, true>("soa L2 G2 packed env", B, E, bytes);
+        run<2, 2, false>("soa L2 G2", B, E, bytes);
         run<1, 1, true>("soa L1 packed env", B, E, bytes);
+        run_pair<1, 0>("pair L1", B, E, bytes);
+        run_pair<2, 0>("pair L2", B, E, bytes);
+        run_pair<2, 1>("pair L2 done lines", B, E, bytes);
+        run_planes<4>("planes 4 B", cin, cout);
+        run_planes<8>("planes 8 B", cin, cout);
+        run_planes<16>("planes 16 B", cin, cout);
     }
     return 0;
 }
