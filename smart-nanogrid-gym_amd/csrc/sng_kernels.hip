@@ -1083,11 +1083,12 @@ struct WideGroup {
     }
 };
 
-// Groups of envs per wavefront of the wide kernel (G): the headline's N = 10 steps two groups of 32 envs per
-// wavefront (1,024 wavefronts at 65,536 envs, one per SIMD), so one group's arithmetic and stores overlap
-// the other's loads; config 5's N = 50 keeps one group (its registers are full at two waves per SIMD).
+// Groups of envs per wavefront of the wide kernel (G, an A/B knob): G = 2 steps two groups of 32 envs per
+// wavefront (1,024 wavefronts at 65,536 envs, one per SIMD), each group's loads issued before the first group
+// is stepped.  Measured at N = 10 (A/B on one box, profiles/r04_ab_groups.txt): 8.62-8.64 us per step in the
+// graph against 6.68-6.71 us with one group (two wavefronts per SIMD), so one group is the default.
 #ifndef SNG_WIDE_G10
-#define SNG_WIDE_G10 2
+#define SNG_WIDE_G10 1
 #endif
 __host__ __device__ constexpr int wide_groups(int NC) { return NC == 10 ? SNG_WIDE_G10 : 1; }
 __host__ __device__ constexpr int wide_waves(int L, int G) {

@@ -1,5 +1,5 @@
-"""GPU: the step kernel the headline bench times -- `void sng::step_wide_kernel<10, 2, 2, true, false, false>`
-(N = 10, two lanes per env, two groups of 32 envs per wavefront, no diagnostics, NumPy-2 / power-of-two dt fast path, packed device-RNG day
+"""GPU: the step kernel the headline bench times -- `void sng::step_wide_kernel<10, 2, 1, true, false, false>`
+(N = 10, two lanes per env, one group of 32 envs per wavefront, no diagnostics, NumPy-2 / power-of-two dt fast path, packed device-RNG day
 records) -- pinned directly to the CPU oracle.
 
 Device-RNG days (GPU generator, as in the bench) are exported in the reference's initial_values layout

@@ -178,7 +178,7 @@ __global__ __launch_bounds__(64) void step_soa(const float *__restrict__ act, fl
 // BESS and day return packed [E][2].  L = 1: a lane per env, every charger load 16 B (8 B for the last record
 // plane); L = 2: part 0 steps chargers 0-3 and 8, part 1 4-7 and 9.  DONE: 0 every lane stores its env's
 // byte, 1 the done bytes are written as whole 128 B lines by every fourth 32-env group (done is uniform).
-template <int L, int DONE>
+template <int L, int DONE, bool SOA_REC = false>
 __global__ __launch_bounds__(64) void step_pair(const float *__restrict__ act, float *__restrict__ obs,
                                                 const uint32_t *__restrict__ rec, double *__restrict__ soc,
                                                 const double *__restrict__ ratio, double *__restrict__ st2,
@@ -207,6 +207,13 @@ __global__ __launch_bounds__(64) void step_pair(const float *__restrict__ act, f
     const v2d *sp = reinterpret_cast<const v2d *>(soc);
     const v4u *rq = reinterpret_cast<const v4u *>(rec_t);
     const uint32_t *r2 = rec_t + 8 * E;
+    if (SOA_REC) {   // records stay [N][E] (only the SoC in charger pairs)
+#pragma unroll
+        for (int j = 0; j < CP; ++j) {
+            const int c = L == 1 ? j : (j < 4 ? 4 * part + j : 8 + part);
+            w[j] = rec_t[(size_t)c * E + e];
+        }
+    }
     if (L == 1) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) {
@@ -214,13 +221,15 @@ __global__ __launch_bounds__(64) void step_pair(const float *__restrict__ act, f
             s[2 * k] = x.x;
             s[2 * k + 1] = x.y;
         }
+        if (!SOA_REC) {
 #pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const v4u x = rq[(size_t)k * E + e];
-            w[4 * k] = x.x, w[4 * k + 1] = x.y, w[4 * k + 2] = x.z, w[4 * k + 3] = x.w;
+            for (int k = 0; k < 2; ++k) {
+                const v4u x = rq[(size_t)k * E + e];
+                w[4 * k] = x.x, w[4 * k + 1] = x.y, w[4 * k + 2] = x.z, w[4 * k + 3] = x.w;
+            }
+            const uint2 y = reinterpret_cast<const uint2 *>(r2)[e];
+            w[8] = y.x, w[9] = y.y;
         }
-        const uint2 y = reinterpret_cast<const uint2 *>(r2)[e];
-        w[8] = y.x, w[9] = y.y;
     } else {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
@@ -229,9 +238,11 @@ __global__ __launch_bounds__(64) void step_pair(const float *__restrict__ act, f
             s[2 * k + 1] = x.y;
         }
         s[4] = soc[(size_t)8 * E + 2 * e + part];
-        const v4u x = rq[(size_t)part * E + e];
-        w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w;
-        w[4] = r2[2 * e + part];
+        if (!SOA_REC) {
+            const v4u x = rq[(size_t)part * E + e];
+            w[0] = x.x, w[1] = x.y, w[2] = x.z, w[3] = x.w;
+            w[4] = r2[2 * e + part];
+        }
     }
 #pragma unroll
     for (int k = 0; k < KA; ++k) {
@@ -437,16 +448,16 @@ __global__ __launch_bounds__(64) void copy_planes(const char *__restrict__ in, c
         __builtin_nontemporal_store(k < NR ? v[k] : acc, reinterpret_cast<vu *>(out + (size_t)k * PLANE + off % PLANE));
 }
 
-template <int L, int DONE>
+template <int L, int DONE, bool SOA_REC = false>
 void run_pair(const char *name, const Bufs &B, int64_t E, double bytes) {
     constexpr int WE = 64 / L;
     const dim3 grid((unsigned)(E / WE)), block(64);
     const size_t lds = (size_t)(WE * A + WE * O) * 4;
-    CK(hipFuncSetAttribute((const void *)step_pair<L, DONE>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    CK(hipFuncSetAttribute((const void *)step_pair<L, DONE, SOA_REC>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     time_it(
         name,
         [&](int t, hipEvent_t a, hipEvent_t b) {
-            hipExtLaunchKernelGGL((step_pair<L, DONE>), grid, block, lds, 0, a, b, 0u, B.act + (size_t)t * E * A,
+            hipExtLaunchKernelGGL((step_pair<L, DONE, SOA_REC>), grid, block, lds, 0, a, b, 0u, B.act + (size_t)t * E * A,
                                   B.obs, B.rec, B.soc, B.ratio, B.st2, B.reward, B.done, B.flags, E, t);
         },
         bytes);
@@ -524,6 +535,8 @@ int main() {
         run_pair<1, 0>("pair L1", B, E, bytes);
         run_pair<2, 0>("pair L2", B, E, bytes);
         run_pair<2, 1>("pair L2 done lines", B, E, bytes);
+        run_pair<2, 0, true>("soc pairs L2, rec soa", B, E, bytes);
+        run_pair<1, 0, true>("soc pairs L1, rec soa", B, E, bytes);
         run_planes<4>("planes 4 B", cin, cout);
         run_planes<8>("planes 8 B", cin, cout);
         run_planes<16>("planes 16 B", cin, cout);
