@@ -1332,7 +1332,7 @@ int sng_get_vehicle_soc(SngEnv *env, double *h, void *stream) {
     HIP_TRY(env, hipSetDevice(env->device));
     const int N = env->p.n;
     hipStream_t st = as_stream(stream);
-    // [N][E] on the device -> [E][N] on the host
+    // charger pairs on the device (sng_layout.h soc_index) -> [E][N] on the host
     std::vector<double> tmp((size_t)N * env->E);
     HIP_TRY(env, hipMemcpyAsync(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost, st));
     // a packed day: an empty charger's running SoC carries the next arrival's (sng_layout.h); SOC[c, t]
@@ -1347,8 +1347,8 @@ int sng_get_vehicle_soc(SngEnv *env, double *h, void *stream) {
     HIP_TRY(env, hipStreamSynchronize(st));
     for (int64_t e = 0; e < env->E; ++e)
         for (int c = 0; c < N; ++c) {
-            const size_t i = (size_t)c * env->E + e;
-            h[e * N + c] = (packed_mid && !(rec[i] & W_OCC)) ? 0.0 : tmp[i];
+            const size_t i = (size_t)c * env->E + e;   // the record plane; the SoC state is in charger pairs
+            h[e * N + c] = (packed_mid && !(rec[i] & W_OCC)) ? 0.0 : tmp[soc_index(c, e, N, env->E)];
         }
     return SNG_OK;
 }
@@ -1372,8 +1372,8 @@ int sng_set_vehicle_soc(SngEnv *env, const double *h, void *stream) {
     }
     for (int64_t e = 0; e < env->E; ++e)
         for (int c = 0; c < N; ++c) {
-            const size_t i = (size_t)c * env->E + e;
-            if (!packed_mid || (rec[i] & W_OCC)) tmp[i] = h[e * N + c];
+            const size_t i = (size_t)c * env->E + e;   // the record plane; the SoC state is in charger pairs
+            if (!packed_mid || (rec[i] & W_OCC)) tmp[soc_index(c, e, N, env->E)] = h[e * N + c];
         }
     HIP_TRY(env, hipMemcpyAsync(env->ds.soc, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipStreamSynchronize(st));
@@ -1486,7 +1486,7 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 
 // ---------------------------------------------------------------------------------
 // Checkpoint / resume: header, then the sections in this order (host byte order):
-//   soc f64[N][E] | bess, bess0, ratio, pen0 f64[E] | flags u32[E] | [word u32[T][N][E], host days]
+//   soc f64[N/2][E][2] (charger pairs) | bess, bess0, ratio, pen0 f64[E] | flags u32[E] | [word u32[T][N][E], host days]
 //   | aux 8B[T][N][E] (a packed day: its u32[T+1][N][E] records, sng_layout.h) | [req f64[T][N][E]]
 //   | [prof f64[2][T+3][E]] | [episode return f64[E]]
 //   | [reference streams u32[E][2][625]]
@@ -1506,8 +1506,9 @@ struct StateHeader {
     uint64_t total_bytes;
 };
 // the last byte is the checkpoint format version: '3' since the configuration fingerprint is hashed
-// field by field (round 3); a blob of another version is refused as such
-static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '3'};
+// field by field (round 3), '4' since the SoC state is stored in charger pairs (round 4); a blob of another
+// version is refused as such
+static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '4'};
 
 // The blob's size for this handle and the header's section flags.
 static uint64_t state_bytes(const SngEnv *env, const StateHeader &h) {

@@ -167,6 +167,35 @@ __device__ __forceinline__ void bst(T *base, uint32_t voff, T v, uint32_t soff =
     else
         __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(unsigned char, v), rsrc(base), voff, soff, POL);
 }
+// Two f64 in one 16 B buffer access (a charger pair of the SoC state, sng_layout.h).
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+template <int POL = 0>
+__device__ __forceinline__ void bld2(const double *base, uint32_t voff, uint32_t soff, double &a, double &b) {
+    const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), voff, soff, POL);
+    a = __builtin_bit_cast(double, (uint64_t)x.x | ((uint64_t)x.y << 32));
+    b = __builtin_bit_cast(double, (uint64_t)x.z | ((uint64_t)x.w << 32));
+}
+// The wave-uniform offset goes into the V# base, not the soffset field: a MUBUF store of more than 8 B reads
+// its data VGPRs a cycle late, and the compiler (ROCm 7.2 LLVM) inserts the wait state a VALU write of those
+// VGPRs needs only when soffset is not a register.  gfx950 needs it either way: with an SGPR soffset, a
+// v_cvt writing the pair's high dword right after the store corrupted ~0.1 % of the stored SoC slots at
+// 65,536 envs (two waves per SIMD; tests/test_gpu_bench_kernel.py, tools/dbg/pairs_dbg.py).
+template <int POL = 0>
+__device__ __forceinline__ void bst2(double *base, uint32_t voff, double a, double b, uint32_t soff = 0) {
+    const uint64_t ua = __builtin_bit_cast(uint64_t, a), ub = __builtin_bit_cast(uint64_t, b);
+    const v4u x = {(unsigned)ua, (unsigned)(ua >> 32), (unsigned)ub, (unsigned)(ub >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(x, rsrc(reinterpret_cast<char *>(base) + soff), voff, 0, POL);
+}
+// Byte offset of charger c of the env whose 8 B slot offset is el8 (8 * env) in the SoC state (charger
+// pairs, sng_layout.h soc_index), split into the per-lane part (v) and the wave-uniform part (s).
+struct SocOff {
+    uint32_t v, s;
+};
+__device__ __forceinline__ SocOff soc_off(int c, int n, int64_t E, uint32_t el8) {
+    const int c0 = c & ~1;
+    const bool two = c0 + 2 <= n;
+    return {two ? 2u * el8 : el8, (uint32_t)c0 * (uint32_t)E * 8u + (two ? (uint32_t)(c & 1) * 8u : 0u)};
+}
 
 // Copy `count` floats global -> LDS with 16 B per lane when the run is aligned.  Each thread
 // issues up to K loads before the first LDS write (clamped, unconditional loads: no per-element
@@ -672,18 +701,26 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
     double aux[NC], run[NC], req[NC];
     const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
 #pragma unroll
-    for (int c = 0; c < NC; ++c) {
-        const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
-        if (PK) {   // packed device-day record (sng_layout.h): plane t + 1
-            w[c] = bld(rec_t, el4, r4);
-        } else {
-            w[c] = bld(s.word + plane, el4, r4);
-            aux[c] = bld(s.aux + plane, el8, r8);
+    for (int c0 = 0; c0 < NC; c0 += 2) {   // charger pairs: the SoC state's 16 B slots (sng_layout.h)
+#pragma unroll
+        for (int c = c0; c < c0 + 2 && c < NC; ++c) {
+            const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
+            if (PK) {   // packed device-day record (sng_layout.h): plane t + 1
+                w[c] = bld(rec_t, el4, r4);
+            } else {
+                w[c] = bld(s.word + plane, el4, r4);
+                aux[c] = bld(s.aux + plane, el8, r8);
+            }
         }
-        run[c] = bld(s.soc, el8, r8);
+        if (c0 + 1 < NC)
+            bld2(s.soc, 2u * el8, (uint32_t)c0 * (uint32_t)E * 8u, run[c0], run[c0 + 1]);
+        else
+            run[c0] = bld(s.soc, el8, (uint32_t)c0 * (uint32_t)E * 8u);
         // Requested_SOC[c, t-1]; without the stream 1.0 (charging_station.py:230-232), or the cleared
         // 0.0 of a replayed day (Params::req_zero)
-        req[c] = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
+#pragma unroll
+        for (int c = c0; c < c0 + 2 && c < NC; ++c)
+            req[c] = REQ ? bld(s.req + plane, el8, (uint32_t)c * (uint32_t)E * 8u) : (p.req_zero ? 0.0 : 1.0);
     }
     act_tile.commit(s_act, lane);
     wave_lds_fence();
@@ -700,7 +737,7 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
     // the header needs only the PV ratio and the constants: written while the chargers' loads fly
     if (live) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, one4, one4);
 
-    double pwv[NC];
+    double pwv[NC], sv[NC];
     double pen_v = 0.0, seq_pos = 0.0, seq_neg = 0.0, pmin = __builtin_inf();
     int n_pos = 0, n_neg = 0;
     uint32_t n_nonexist = 0, fl = 0;
@@ -714,7 +751,11 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
             const bool occ = (w[c] & W_OCC) != 0;
             const ChargerResult r = charger_step<true, true>(p, PK ? (w[c] & ~W_STATIC) : w[c], PK ? 0.0 : aux[c], run[c],
                                                              req[c], av[c], t, recip_cap((double)capi));
-            bst<kNT>(s.soc, el8, (PK && !occ) ? (double)rec_soc(w[c]) : r.soc, (uint32_t)c * (uint32_t)E * 8u);
+            sv[c] = (PK && !occ) ? (double)rec_soc(w[c]) : r.soc;
+            if (c & 1)   // the pair's 16 B slot once both chargers are stepped
+                bst2<kNT>(s.soc, 2u * el8, sv[c - 1], sv[c], (uint32_t)(c - 1) * (uint32_t)E * 8u);
+            else if (c == NC - 1)
+                bst<kNT>(s.soc, el8, sv[c], (uint32_t)c * (uint32_t)E * 8u);
             o_row[k_soc + c] = (float)r.soc;
             o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[c]);
             n_nonexist += r.nx;
@@ -856,26 +897,38 @@ struct WideGroup {
     static constexpr int WENVS = Lay::WENVS, CPL = (NC + L - 1) / L;
     static constexpr int KT = (Lay::A * WENVS + 4 * kWave - 1) / (4 * kWave);
     static_assert((L - 1) * CPL < NC, "every lane steps at least one charger");
+    // The lane's chargers.  Two lanes and N = 2 mod 4 (the headline's 10, config 5's 50): lane `part` steps the
+    // whole charger pairs [part H, part H + H) (H = (N - 2) / 2) and charger N - 2 + part of the last pair, so
+    // its SoC state moves as 16 B charger pairs (sng_layout.h) but for that last charger.  Otherwise the
+    // contiguous ranges [part CPL, min(N, part CPL + CPL)).
+    static constexpr bool kPairs = L == 2 && NC % 4 == 2;
+    static constexpr int H = (NC - 2) / 2;
+    static_assert(!kPairs || CPL == H + 1, "a lane's chargers: H from whole pairs and one from the last");
+    static __device__ __forceinline__ int charger(int part, int j) {
+        return kPairs ? (j < H ? part * H + j : NC - 2 + part) : part * CPL + j;
+    }
     int64_t e0;
     int nw;
     bool live;
-    uint32_t el1, el4, el8, row4, row4_last;
+    uint32_t el1, el4, el8, row4, row4_last, soc_a, soc_b;
     TileStage<KT, kWave> act_tile;
     double ratio, bess_l, pen0_l, ret_l;
     double fpv[4], fpr[4];
     uint32_t w[CPL];
     double aux[PK ? 1 : CPL], run_[CPL], req[REQ ? CPL : 1];
 
-    // the (per-lane, uniform) byte offsets of charger j of the lane: j * E in the uniform part, except for
-    // the j some lane lacks (a ragged last lane), where the per-lane part carries it
-    static __device__ __forceinline__ bool ragged(int j) { return NC % L != 0 && j >= NC - (L - 1) * CPL; }
+    // the (per-lane, uniform) byte offsets of charger j of the lane in a [N][E] u32 plane: j * E in the uniform
+    // part, except for the j some lane lacks (a ragged last lane) or the last pair's charger, where the
+    // per-lane part carries it
+    static __device__ __forceinline__ bool ragged(int j) { return !kPairs && NC % L != 0 && j >= NC - (L - 1) * CPL; }
     __device__ __forceinline__ uint32_t r4_of(int j, int64_t E) const {
+        if constexpr (kPairs) return (uint32_t)(j < H ? j : NC - 2) * (uint32_t)E * 4u;
         return ragged(j) ? 0u : (uint32_t)j * (uint32_t)E * 4u;
     }
     __device__ __forceinline__ uint32_t row_of(int j, int nc, int64_t E) const {
+        if constexpr (kPairs) return j < H ? row4 : row4_last;
         return ragged(j) ? (j < nc ? row4 + (uint32_t)j * (uint32_t)E * 4u : row4_last) : row4;
     }
-
     // loads oldest-needed-first: the actions tile and the per-env values, then every charger's state
     __device__ __forceinline__ void issue(int64_t e0_, const float *act, int64_t E, int t, int vec_io, const Params &p,
                                           const DeviceState &s, const InfoPtrs &info, int lane) {
@@ -888,11 +941,19 @@ struct WideGroup {
         el4 = el1 * 4u;
         el8 = el1 * 8u;
         const int c0 = part * CPL;
-        const int nc = (NC - c0) < CPL ? NC - c0 : CPL;
-        // the lane's first charger row as a per-lane byte offset; charger j of the lane adds j * E (uniform).
-        // Past the lane's range (j >= nc) the loads re-read its first charger and nothing is stored.
-        row4 = el4 + (uint32_t)c0 * (uint32_t)E * 4u;
-        row4_last = el4 + (uint32_t)(NC - 1) * (uint32_t)E * 4u;
+        const int nc = kPairs ? CPL : ((NC - c0) < CPL ? NC - c0 : CPL);
+        if constexpr (kPairs) {
+            row4 = el4 + (uint32_t)(part * H) * (uint32_t)E * 4u;     // charger part H + j, j < H: + j E (uniform)
+            row4_last = el4 + (uint32_t)part * (uint32_t)E * 4u;      // charger N - 2 + part: + (N - 2) E (uniform)
+            soc_a = 2u * el8 + (uint32_t)(part * H) * (uint32_t)E * 8u;   // pair row part H + j: + j E 8 (uniform)
+            soc_b = 2u * el8 + (uint32_t)part * 8u;                      // the last pair's row: + (N - 2) E 8
+        } else {
+            // the lane's first charger row as a per-lane byte offset; charger j of the lane adds j * E
+            // (uniform).  Past the lane's range (j >= nc) the loads re-read its first charger and nothing is
+            // stored.
+            row4 = el4 + (uint32_t)c0 * (uint32_t)E * 4u;
+            row4_last = el4 + (uint32_t)(NC - 1) * (uint32_t)E * 4u;
+        }
         const size_t plane = (size_t)t * NC * (size_t)E;   // this step's timeline planes
         const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
         const int Ad = p.act_dim;
@@ -913,7 +974,7 @@ struct WideGroup {
         }
 #pragma unroll
         for (int j = 0; j < CPL; ++j) {
-            // charger c0 + j (past a ragged lane's range: its charger NC - 1 again, discarded)
+            // charger `charger(part, j)` (past a ragged lane's range: its charger NC - 1 again, discarded)
             const uint32_t v4 = row_of(j, nc, E), r4 = r4_of(j, E), v8 = 2u * v4, r8 = 2u * r4;
             if (PK) {
                 w[j] = bld(rec_t, v4, r4);
@@ -921,7 +982,13 @@ struct WideGroup {
                 w[j] = bld(s.word + plane, v4, r4);
                 aux[PK ? 0 : j] = bld(s.aux + plane, v8, r8);
             }
-            run_[j] = bld(s.soc, v8, r8);
+            if constexpr (kPairs) {   // a pair's 16 B once both its records are issued; the last pair's 8 B
+                if (j < H && (j & 1)) bld2(s.soc, soc_a, (uint32_t)(j - 1) * (uint32_t)E * 8u, run_[j - 1], run_[j]);
+                if (j == H) run_[j] = bld(s.soc, soc_b, (uint32_t)(NC - 2) * (uint32_t)E * 8u);
+            } else {
+                const int c = c0 + j < NC ? c0 + j : NC - 1;
+                run_[j] = bld(s.soc, (uint32_t)soc_index(c, el, NC, E) * 8u);
+            }
             if (REQ) req[REQ ? j : 0] = bld(s.req + plane, v8, r8);
         }
     }
@@ -938,7 +1005,7 @@ struct WideGroup {
         const int le = lane / L, part = lane % L;
         const bool leader = part == 0;
         const int c0 = part * CPL;
-        const int nc = (NC - c0) < CPL ? NC - c0 : CPL;
+        const int nc = kPairs ? CPL : ((NC - c0) < CPL ? NC - c0 : CPL);
         const size_t plane = (size_t)t * NC * (size_t)E;
         const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;
         const float *a_row = s_act + le * Ad;
@@ -947,7 +1014,8 @@ struct WideGroup {
         float amin = 0.0f;
 #pragma unroll
         for (int j = 0; j < CPL; ++j) {
-            av[j] = a_row[(c0 + j) < NC ? c0 + j : NC - 1];
+            const int c = charger(part, j);
+            av[j] = a_row[c < NC ? c : NC - 1];
             amin = __builtin_fminf(amin, av[j]);   // a NaN action is not negative (fmin drops it)
         }
         const float bess_action = p.bess ? a_row[NC] : 0.0f;
@@ -960,12 +1028,12 @@ struct WideGroup {
             // the fast loop: no negative action in the wave, so no negative power (p_dis stays 0.0)
             double seq_pos = 0.0, pmin = __builtin_inf();
             int n_pos = 0;
-            double qv[L > 1 ? CPL : 1];
+            double qv[L > 1 ? CPL : 1], sv[CPL];
             if (live) {
 #pragma unroll
                 for (int j = 0; j < CPL; ++j) {
-                    const int c = c0 + j;
-                    if (NC % L != 0 && j >= nc) {   // a ragged lane's range ends: adds nothing
+                    const int c = charger(part, j);
+                    if (!kPairs && NC % L != 0 && j >= nc) {   // a ragged lane's range ends: adds nothing
                         qv[L > 1 ? j : 0] = 0.0;
                         continue;
                     }
@@ -974,14 +1042,22 @@ struct WideGroup {
                     const ChargerResult r = charger_step<true, true>(p, PK ? (w[j] & ~W_STATIC) : w[j],
                                                                      PK ? 0.0 : aux[PK ? 0 : j], run_[j], req_of(j, p), av[j],
                                                                      t, recip_cap((double)capi));
-                    bst<kNT>(s.soc, 2u * row_of(j, nc, E), (PK && !occ) ? (double)rec_soc(w[j]) : r.soc,
-                             2u * r4_of(j, E));
+                    sv[j] = (PK && !occ) ? (double)rec_soc(w[j]) : r.soc;
+                    if constexpr (kPairs) {   // a pair's 16 B once both its chargers are stepped; the last pair's 8 B
+                        if (j < H && (j & 1))
+                            bst2<kNT>(s.soc, soc_a, sv[j - 1], sv[j], (uint32_t)(j - 1) * (uint32_t)E * 8u);
+                        if (j == H) bst<kNT>(s.soc, soc_b, sv[j], (uint32_t)(NC - 2) * (uint32_t)E * 8u);
+                    } else {
+                        bst<kNT>(s.soc, (uint32_t)soc_index(c, el1, NC, E) * 8u, sv[j]);
+                    }
                     o_row[k_soc + c] = (float)r.soc;
                     o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[j]);
                     n_nonexist += r.nx;
                     fl |= r.fl;
                     if (L > 1) qv[L > 1 ? j : 0] = r.q;
-                    pen_v += r.q;
+                    // the lane's own penalties in charger order; kPairs: the last pair's come after the other
+                    // lane's whole pairs (gather, below)
+                    if (!kPairs || j < H) pen_v += r.q;
                     const bool ip = r.pw > 0.0;
                     seq_pos += __builtin_fmax(r.pw, 0.0);
                     n_pos += ip ? 1 : 0;
@@ -1010,7 +1086,7 @@ struct WideGroup {
                     n_nonexist += from_part<L, K>(nx_own);
                     fl |= from_part<L, K>(fl_own);
 #pragma unroll
-                    for (int j = 0; j < CPL; ++j) {
+                    for (int j = 0; j < (kPairs ? H : CPL); ++j) {
                         const double qk = from_part<L, K>(qv[L > 1 ? j : 0]);
                         pen_v = leader ? pen_v + qk : pen_v;
                     }
@@ -1019,6 +1095,10 @@ struct WideGroup {
                 if constexpr (L > 2) {
                     gather(std::integral_constant<int, 2>{});
                     gather(std::integral_constant<int, 3>{});
+                }
+                if constexpr (kPairs) {   // the last pair: charger N - 2 (this lane), then N - 1 (the other)
+                    const double qk = from_part<L, 1>(qv[L > 1 ? H : 0]);
+                    pen_v = leader ? (pen_v + qv[L > 1 ? H : 0]) + qk : pen_v;
                 }
                 split = with_pos > 1;
             }
@@ -1051,15 +1131,16 @@ struct WideGroup {
 #pragma unroll 1
                 for (int c = 0; c < NC; ++c) {
                     const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
+                    const SocOff so = soc_off(c, NC, E, el8);
                     const uint32_t wc = PK ? bld(rec_t, el4, r4) : bld(s.word + plane, el4, r4);
                     const double auxc = PK ? 0.0 : bld(s.aux + plane, el8, r8);
-                    const double runc = bld(s.soc, el8, r8);
+                    const double runc = bld(s.soc, so.v, so.s);
                     const double reqc = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
                     const uint32_t capi = (wc >> W_CAP_SHIFT) & 0xffu;
                     const bool occ = (wc & W_OCC) != 0;
                     const ChargerResult r = charger_step<true, true>(p, PK ? (wc & ~W_STATIC) : wc, auxc, runc, reqc,
                                                                      a_row[c], t, recip_cap((double)capi));
-                    bst<kNT>(s.soc, el8, (PK && !occ) ? (double)rec_soc(wc) : r.soc, r8);
+                    bst<kNT>(s.soc, so.v, (PK && !occ) ? (double)rec_soc(wc) : r.soc, so.s);
                     o_row[k_soc + c] = (float)r.soc;
                     o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : wc);
                     n_nonexist += r.nx;
@@ -1217,7 +1298,8 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
                     w[j] = bld(word_t, el4, r4);
                     aux[j] = bld(aux_t, el8, r8);
                 }
-                run[j] = bld(socv, el8, r8);
+                const SocOff so = soc_off(c, n, E, el8);   // the SoC state in charger pairs
+                run[j] = bld(socv, so.v, so.s);
             } else {
                 w[j] = 0u;
                 aux[j] = run[j] = 0.0;
@@ -1268,7 +1350,8 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
                     wn[j] = bld(word_t, el4, r4);
                     auxn[j] = bld(aux_t, el8, r8);
                 }
-                runn[j] = bld(socv, el8, r8);
+                const SocOff so = soc_off(c, n, E, el8);
+                runn[j] = bld(socv, so.v, so.s);
                 reqn[j] = rq_live ? bld(req_t, el8, r8) : rq;
             }
         }
@@ -1406,7 +1489,8 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
 #else
                 const ChargerResult r = charger_step<FAST, true>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
 #endif
-                bst<kNT>(socv, el8, (PK && !occ) ? (double)rec_soc(w[j]) : r.soc, (uint32_t)c * (uint32_t)E * 8u);
+                const SocOff so = soc_off(c, n, E, el8);
+                bst<kNT>(socv, so.v, (PK && !occ) ? (double)rec_soc(w[j]) : r.soc, so.s);
                 if (DIAG) {   // 'Charger power values' and the SOC[c, t] the day record holds
                     if (info.charger_power) info.charger_power[(size_t)e * n + c] = r.pw;
                     if (info.vehicle_soc) info.vehicle_soc[(size_t)e * n + c] = r.soc;
@@ -1650,7 +1734,11 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
             for (int j = 0; j < B; ++j) {
                 const int c = c0 + j;
                 if (c < n) {
-                    SNG_ST(socv[(size_t)c * E + e], aux[j]);
+                    // the SoC state in charger pairs (sng_layout.h): one 16 B store per pair (c0 is even)
+                    if (c + 1 < n && !(j & 1))
+                        bst2<kNT>(socv, (uint32_t)soc_index(c, e, n, E) * 8u, aux[j], aux[j + 1 < B ? j + 1 : j]);
+                    else if (c + 1 == n && !(j & 1))
+                        bst<kNT>(socv, (uint32_t)soc_index(c, e, n, E) * 8u, aux[j]);
                     o_row[k + c] = (float)aux[j];
                     o_row[k + n + c] = departure_obs(w[j]);
                 }
@@ -1815,14 +1903,25 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
         }
         const int k = p.pv ? 8 : 4;
         const uint32_t el8 = (uint32_t)e * 8u;
-        for (int c = part - 1; part > 0 && c < n; c += kObsParts - 1) {
-            GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
-            const VehicleDraw d = draw_vehicle(p, rng, 0, i4, i10, i1);
-            const bool occ0 = d.ta == 0;   // t = 0 < T always, and dep >= 4/dt > 0
-            const double soc0 = occ0 ? d.soc : 0.0;
-            bst<kNT>(s.soc, el8, soc0, (uint32_t)c * (uint32_t)E * 8u);
-            o_row[k + c] = (float)soc0;
-            o_row[k + n + c] = departure_obs(pack_word(occ0, occ0, false, 0u, occ0 ? (uint32_t)d.dep : 0u));
+        // wavefronts 1..3: charger pairs part - 1, part + 2, ... (the SoC state's 16 B slots, sng_layout.h)
+        for (int c0 = 2 * (part - 1); part > 0 && c0 < n; c0 += 2 * (kObsParts - 1)) {
+            double soc0[2] = {0.0, 0.0};
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int c = c0 + i;
+                if (c >= n) break;
+                GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
+                const VehicleDraw d = draw_vehicle(p, rng, 0, i4, i10, i1);
+                const bool occ0 = d.ta == 0;   // t = 0 < T always, and dep >= 4/dt > 0
+                soc0[i] = occ0 ? d.soc : 0.0;
+                o_row[k + c] = (float)soc0[i];
+                o_row[k + n + c] = departure_obs(pack_word(occ0, occ0, false, 0u, occ0 ? (uint32_t)d.dep : 0u));
+            }
+            const SocOff so = soc_off(c0, n, E, el8);
+            if (c0 + 1 < n)
+                bst2<kNT>(s.soc, so.v, soc0[0], soc0[1], so.s);
+            else
+                bst<kNT>(s.soc, so.v, soc0[0], so.s);
         }
     }
     __syncthreads();

@@ -3,7 +3,10 @@
 // State of arrays, env index fastest everywhere so a wavefront's 64 lanes (64 envs)
 // touch one contiguous 256 B / 512 B run per charger:
 //
-//   soc    f64 [N][E]       SOC[c, t] of the last stepped timestep (charger.py:16 array, one slot)
+//   soc    f64 [N/2][E][2]  SOC[c, t] of the last stepped timestep (charger.py:16 array, one slot), in charger
+//                           pairs: chargers 2k and 2k + 1 of env e are the 16 B at pair k's row, slot e, so a
+//                           lane moves two of its env's chargers in one 16 B access (a wavefront: one 1 KiB run
+//                           per instruction); with N odd the last charger is a row [E] of its own (soc_index)
 //   bess   f64 [E]          BESS state of charge (persists across days)
 //   bess0  f64 [E]          'Initial battery state of charge' of the current day
 //   ratio  f64 [E]          random_pv_shift_ratio of the current day
@@ -66,6 +69,13 @@ constexpr int kPriceLen = 48;       // accountant.py:14, 49 (2T with the extende
 SNG_HD inline uint32_t pack_word(bool occ, bool stat, bool pen, uint32_t cap, uint32_t dep) {
     return (occ ? W_OCC : 0u) | (stat ? W_STATIC : 0u) | (pen ? W_PEN : 0u) | ((cap & 0xffu) << W_CAP_SHIFT) |
            ((dep & 0xffu) << W_DEP_SHIFT);
+}
+
+// Element index of charger c, env e in the SoC state (charger pairs, above): pair row c & ~1 holds E
+// 16 B slots, a last unpaired charger (N odd) a row of E 8 B slots.
+SNG_HD inline size_t soc_index(int c, int64_t e, int n, int64_t E) {
+    const int c0 = c & ~1;
+    return (size_t)c0 * (size_t)E + (c0 + 2 <= n ? (size_t)e * 2u + (size_t)(c & 1) : (size_t)e);
 }
 
 constexpr int REC_SOC_SHIFT = 3;
