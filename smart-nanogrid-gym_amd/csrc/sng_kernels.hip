@@ -408,7 +408,11 @@ struct ChargerResult {
 // (validated when a scenario is encoded).
 // FAST (NumPy-2 promotion and dt a power of two, e.g. the 1 h default) is straight-line code, so the
 // compiler interleaves the chargers of an env.
-template <bool FAST, bool RCP>
+// NONNEG: the caller knows a >= +0.0 (not NaN, not -0.0): the wide kernel's fast loop, which a wavefront
+// takes only when none of its actions is negative, -0.0 or NaN.  Then a vehicle either charges (a > 0) or idles, so the discharge
+// branch -- the inverted-flag power (charger.py:122-132) and max(0, calc) -- is never selected and is not
+// computed; every value this returns equals the general form's for such actions.
+template <bool FAST, bool RCP, bool NONNEG = false>
 __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, double req,
                                                       float a, int t, double rcap) {
     ChargerResult o;
@@ -446,6 +450,14 @@ __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t 
         change = RCP ? div_by_cap((double)pdt, cap, rcap) : (double)pdt / cap;
     }
     const double calc = prev + change;
+    if constexpr (NONNEG) {   // a > 0 charges, a == 0 idles (chg == !idle)
+        const bool moved = occ && chg && p.bounded;
+        o.soc = moved ? ((1.0 < calc) ? 1.0 : calc) : prev;
+        o.pw = moved ? pc : 0.0;
+        o.nx = (!occ && chg) ? 1u : 0u;
+        o.fl = (occ && chg && !p.bounded) ? (uint32_t)SNG_FLAG_CHARGING_MODE : 0u;
+        return o;
+    }
     double pw_dis = pc;                                          // inverted flag, charger.py:122-132
     if (FAST) {
         pw_dis = (calc >= 0.0) ? -((prev * cap) * p.rdt) : pc;
@@ -902,6 +914,10 @@ struct WideGroup {
     // its SoC state moves as 16 B charger pairs (sng_layout.h) but for that last charger.  Otherwise the
     // contiguous ranges [part CPL, min(N, part CPL + CPL)).
     static constexpr bool kPairs = L == 2 && NC % 4 == 2;
+    // the fast loop's charger step without the discharge branch (charger_step NONNEG) for the headline's
+    // station; at N = 50 the compiler then merges several chargers' select masks ahead of the per-charger
+    // scheduling barriers and spills them (332 v_readlane), so config 5 keeps the general form
+    static constexpr bool kNonneg = NC <= 16;
     static constexpr int H = (NC - 2) / 2;
     static_assert(!kPairs || CPL == H + 1, "a lane's chargers: H from whole pairs and one from the last");
     static __device__ __forceinline__ int charger(int part, int j) {
@@ -1011,21 +1027,26 @@ struct WideGroup {
         const float *a_row = s_act + le * Ad;
         float *o_row = s_obs + le * O;
         float av[CPL];
-        float amin = 0.0f;
+        // the largest action bit pattern: above +inf's (0x7f800000) when some action is negative (-0.0 too) or
+        // NaN, and such a wavefront takes the general order below (an integer max keeps no per-charger lane
+        // masks alive into the charger loop)
+        uint32_t amax_bits = 0u;
 #pragma unroll
         for (int j = 0; j < CPL; ++j) {
             const int c = charger(part, j);
             av[j] = a_row[c < NC ? c : NC - 1];
-            amin = __builtin_fminf(amin, av[j]);   // a NaN action is not negative (fmin drops it)
+            amax_bits = __builtin_elementwise_max(amax_bits, __builtin_bit_cast(uint32_t, av[j]));
         }
+        const bool not_nonneg = amax_bits > 0x7f800000u;
         const float bess_action = p.bess ? a_row[NC] : 0.0f;
         const int k_soc = p.pv ? 8 : 4;
         if (live && leader) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, fpv, fpr);
 
         double pen_v = 0.0, p_ch = 0.0, p_dis = 0.0;
         uint32_t n_nonexist = 0, fl = 0;
-        if (__builtin_amdgcn_ballot_w64(live && amin < 0.0f) == 0) {
-            // the fast loop: no negative action in the wave, so no negative power (p_dis stays 0.0)
+        if (__builtin_amdgcn_ballot_w64(live && not_nonneg) == 0) {
+            // the fast loop: every action of the wave is >= 0, so no negative power (p_dis stays 0.0) and no
+            // charger discharges (charger_step<..., NONNEG>)
             double seq_pos = 0.0, pmin = __builtin_inf();
             int n_pos = 0;
             double qv[L > 1 ? CPL : 1], sv[CPL];
@@ -1039,9 +1060,9 @@ struct WideGroup {
                     }
                     const uint32_t capi = (w[j] >> W_CAP_SHIFT) & 0xffu;
                     const bool occ = (w[j] & W_OCC) != 0;
-                    const ChargerResult r = charger_step<true, true>(p, PK ? (w[j] & ~W_STATIC) : w[j],
-                                                                     PK ? 0.0 : aux[PK ? 0 : j], run_[j], req_of(j, p), av[j],
-                                                                     t, recip_cap((double)capi));
+                    const ChargerResult r = charger_step<true, true, kNonneg>(p, PK ? (w[j] & ~W_STATIC) : w[j],
+                                                                           PK ? 0.0 : aux[PK ? 0 : j], run_[j], req_of(j, p),
+                                                                           av[j], t, recip_cap((double)capi));
                     sv[j] = (PK && !occ) ? (double)rec_soc(w[j]) : r.soc;
                     if constexpr (kPairs) {   // a pair's 16 B once both its chargers are stepped; the last pair's 8 B
                         if (j < H && (j & 1))
@@ -1059,7 +1080,7 @@ struct WideGroup {
                     // lane's whole pairs (gather, below)
                     if (!kPairs || j < H) pen_v += r.q;
                     const bool ip = r.pw > 0.0;
-                    seq_pos += __builtin_fmax(r.pw, 0.0);
+                    seq_pos += r.pw;   // >= 0 here (the float32 product of a >= 0, or 0.0): adding it is exact
                     n_pos += ip ? 1 : 0;
                     pmin = __builtin_fmin(pmin, ip ? r.pw : __builtin_inf());
                     // chargers in order (groups of kWideSB): charger j waits only for its own loads
