@@ -476,56 +476,75 @@ __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t 
 }
 
 // ---------------------------------------------------------------------------------
-// Env tail: BESS, grid energy, cost, reward (central_management_system.py:99-185,
-// battery_energy_storage_system.py:30-106, penaliser.py:104-111/177-187,
-// accountant.py:26-40) and the observation header.  Leader lane only.
+// The BESS step of an env (central_management_system.py:93-94, battery_energy_storage_system.py:30-106,
+// penaliser.py:104-111): the new SoC (stored), its penalty and powers, and what it adds to the grid
+// balance.  It needs only the BESS SoC and action, not the chargers, so the wide step kernel runs it
+// before the charger loop (while the chargers' loads are in flight); env_tail runs it in place otherwise.
 // ---------------------------------------------------------------------------------
-template <bool DIAG>
+struct BessStep {
+    double bess, pen_b, bpow, bcalc, pw, dp;
+    bool moved, chg;
+    uint32_t fl;
+};
+__device__ __forceinline__ BessStep bess_step(const Params &p, const DeviceState &s, uint32_t el8, int t, double bess,
+                                              float bess_action) {
+    BessStep b{bess, 0.0, 0.0, 0.0, 0.0, 0.0, false, false, 0u};
+    if (!p.bess) return b;
+    if (t == 0) bst(s.bess0, el8, bess);                       // :93-94
+    // charge (ba > 0, battery_energy_storage_system.py:46-74) and discharge (ba < 0, :76-106) share one
+    // select-based path with one division: the two branches differ only in their constants, the
+    // over-discharge clamp and the SoC bound
+    const double ba = (double)bess_action;
+    b.chg = ba > 0.0;
+    b.pw = (ba * (b.chg ? p.bess_pmax_ch : p.bess_pmax_dis)) * (b.chg ? p.bess_eff_ch : p.bess_eff_dis);
+    const double calc = bess + (b.pw * p.dt) / p.bess_cap;
+    const double empty = bess * p.bess_cap;   // the over-discharge clamp's energy
+    b.dp = (calc < 0.0) ? -(p.dt_pow2 ? empty * p.rdt : empty / p.dt) : b.pw;
+    if (ba == 0.0) {
+        b.bpow = 0.0;
+        b.bcalc = 0.0;
+    } else if (!p.bounded) {
+        b.fl |= SNG_FLAG_CHARGING_MODE;
+    } else {
+        b.moved = true;
+        b.bcalc = b.pw;
+        b.bess = b.chg ? ((1.0 < calc) ? 1.0 : calc) : ((calc > 0.0) ? calc : 0.0);
+        b.bpow = b.chg ? b.pw : b.dp;
+    }
+    if (b.bess < p.bess_dod) {                                 // penaliser.py:104-111
+        const double d = (p.bess_dod - b.bess) * 10;
+        b.pen_b = d * d;
+    } else if (!(b.bess <= 1.0)) {
+        b.fl |= SNG_FLAG_BESS_SOC_ABOVE_1;
+    }
+    bst<kNT>(s.bess, el8, b.bess);
+    return b;
+}
+
+// ---------------------------------------------------------------------------------
+// Env tail: BESS (unless PRE: bess_step ran before the chargers), grid energy, cost, reward
+// (central_management_system.py:99-185, penaliser.py:177-187, accountant.py:26-40) and the observation's
+// BESS entry.  Leader lane only.
+// ---------------------------------------------------------------------------------
+template <bool DIAG, bool PRE = false>
 __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, const InfoPtrs &info, int64_t e0, uint32_t lo, uint32_t el1, uint32_t el8,
                                          int t, double ratio, double bess, float bess_action, double p_ch,
                                          double p_dis, double pen_v, double nonexist, uint32_t fl, float *o_row,
                                          const double *cst, const double *fpv, const double *fpr, double ret_prev,
-                                         double bess0, double *__restrict__ reward, uint8_t *__restrict__ done) {
+                                         double bess0, double *__restrict__ reward, uint8_t *__restrict__ done,
+                                         const BessStep *pre = nullptr) {
     // no global loads in here: a load would wait (vmcnt) for every SoC store the env just issued
     const double solar = p.pv ? (cst[CST_PV] * ratio) * fpv[0] : 0.0;   // central_management_system.py:99-103
     const double demand = p_ch + p_dis;                            // :105
     if (demand < 0.0) fl |= p.v2x ? SNG_FLAG_V2X_BREAKPOINT : SNG_FLAG_NEGATIVE_DEMAND;
     double rem = demand - solar;                                   // :167
 
-    double pen_b = 0.0, bpow = 0.0, bcalc = 0.0;
-    if (p.bess) {
-        if (t == 0) {                                              // :93-94
-            bst(s.bess0, el8, bess);
-            bess0 = bess;
-        }
-        // charge (ba > 0, battery_energy_storage_system.py:46-74) and discharge (ba < 0,
-        // :76-106) share one select-based path with one division: the two branches differ only
-        // in their constants, the over-discharge clamp and the SoC bound
-        const double ba = (double)bess_action;
-        const bool chg = ba > 0.0;
-        const double pw = (ba * (chg ? p.bess_pmax_ch : p.bess_pmax_dis)) * (chg ? p.bess_eff_ch : p.bess_eff_dis);
-        const double calc = bess + (pw * p.dt) / p.bess_cap;
-        const double empty = bess * p.bess_cap;   // the over-discharge clamp's energy
-        const double dp = (calc < 0.0) ? -(p.dt_pow2 ? empty * p.rdt : empty / p.dt) : pw;
-        if (ba == 0.0) {
-            bpow = 0.0;
-            bcalc = 0.0;
-        } else if (!p.bounded) {
-            fl |= SNG_FLAG_CHARGING_MODE;
-        } else {
-            bcalc = pw;
-            bess = chg ? ((1.0 < calc) ? 1.0 : calc) : ((calc > 0.0) ? calc : 0.0);
-            bpow = chg ? pw : dp;
-            rem = chg ? -((-rem) - pw) : rem + dp;
-        }
-        if (bess < p.bess_dod) {                                   // penaliser.py:104-111
-            const double d = (p.bess_dod - bess) * 10;
-            pen_b = d * d;
-        } else if (!(bess <= 1.0)) {
-            fl |= SNG_FLAG_BESS_SOC_ABOVE_1;
-        }
-        bst<kNT>(s.bess, el8, bess);
-    }
+    if (p.bess && t == 0) bess0 = bess;
+    const BessStep b = PRE ? *pre : bess_step(p, s, el8, t, bess, bess_action);
+    fl |= b.fl;
+    if (b.moved) rem = b.chg ? -((-rem) - b.pw) : rem + b.dp;     // battery_energy_storage_system.py:46-106
+    const double pen_b = b.pen_b, bpow = b.bpow, bcalc = b.bcalc;
+    bess = b.bess;
 
     const double grid = rem;
     const double energy = grid * p.dt;
@@ -537,7 +556,7 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     bst<kNT>(done, el1, (uint8_t)((t + 1 == p.T) ? 1 : 0));
 
     // (the observation header was written before the chargers: step_kernel)
-    if (p.bess) o_row[p.obs_dim - 1] = (float)bess;
+    if (p.bess && !PRE) o_row[p.obs_dim - 1] = (float)bess;
 
     if (fl) {   // rare (sticky error bits); no-return atomics, nothing waits
         atomicOr(s.flags + e0 + lo, fl);
@@ -1040,7 +1059,14 @@ struct WideGroup {
         const bool not_nonneg = amax_bits > 0x7f800000u;
         const float bess_action = p.bess ? a_row[NC] : 0.0f;
         const int k_soc = p.pv ? 8 : 4;
-        if (live && leader) write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, fpv, fpr);
+        // the observation header and the BESS step need only per-env values: both run here, while the
+        // chargers' loads are still in flight (the BESS's division no longer trails the charger sums)
+        BessStep bs{};
+        if (live && leader) {
+            write_obs_header(o_row, p, k.v + CST_IRR, k.v + CST_PN, ratio, fpv, fpr);
+            bs = bess_step(p, s, el8, t, p.bess ? bess_l : 0.0, bess_action);
+            if (p.bess) o_row[O - 1] = (float)bs.bess;
+        }
 
         double pen_v = 0.0, p_ch = 0.0, p_dis = 0.0;
         uint32_t n_nonexist = 0, fl = 0;
@@ -1176,9 +1202,9 @@ struct WideGroup {
         }
         if (live && leader) {
             pen_v += (t == 0) ? pen0_l : 0.0;   // python index -1 slot; every per-charger term is 0 at t = 0
-            env_tail<false>(p, s, info, e0, (uint32_t)le, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action,
-                            p_ch, p_dis, pen_v, 100.0 * (double)n_nonexist, fl, o_row, k.v, fpv, fpr,
-                            info.episode_return ? ret_l : 0.0, 0.0, reward, done);
+            env_tail<false, true>(p, s, info, e0, (uint32_t)le, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action,
+                                  p_ch, p_dis, pen_v, 100.0 * (double)n_nonexist, fl, o_row, k.v, fpv, fpr,
+                                  info.episode_return ? ret_l : 0.0, 0.0, reward, done, &bs);
         }
         wave_lds_fence();
         copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
