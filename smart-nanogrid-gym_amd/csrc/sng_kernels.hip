@@ -934,9 +934,15 @@ struct WideGroup {
     // contiguous ranges [part CPL, min(N, part CPL + CPL)).
     static constexpr bool kPairs = L == 2 && NC % 4 == 2;
     // the fast loop's charger step without the discharge branch (charger_step NONNEG) for the headline's
-    // station; at N = 50 the compiler then merges several chargers' select masks ahead of the per-charger
-    // scheduling barriers and spills them (332 v_readlane), so config 5 keeps the general form
-    static constexpr bool kNonneg = NC <= 16;
+    // station (step 6.60-6.66 -> 6.53-6.56 us, profiles/r04_ab_nonneg.txt).  At N = 50 the compiler merges
+    // several chargers' select masks ahead of the per-charger scheduling barriers and spills them (332
+    // v_readlane); with each charger's inputs pinned to its block (SNG_WIDE_PIN) it compiles to 5.5 % fewer
+    // VALU, and config 5 ran 22.62-22.69 against 22.47-22.54 us (profiles/r04_ab_config5_nonneg.txt): its
+    // step is bound by its bytes, so config 5 keeps the general form
+#ifndef SNG_NONNEG_MAX
+#define SNG_NONNEG_MAX 16
+#endif
+    static constexpr bool kNonneg = NC <= SNG_NONNEG_MAX;
     static constexpr int H = (NC - 2) / 2;
     static_assert(!kPairs || CPL == H + 1, "a lane's chargers: H from whole pairs and one from the last");
     static __device__ __forceinline__ int charger(int part, int j) {
@@ -1084,6 +1090,9 @@ struct WideGroup {
                         qv[L > 1 ? j : 0] = 0.0;
                         continue;
                     }
+#ifdef SNG_WIDE_PIN
+                    asm volatile("" : "+v"(av[j]), "+v"(w[j]));   // A/B: pin the charger's inputs to its block
+#endif
                     const uint32_t capi = (w[j] >> W_CAP_SHIFT) & 0xffu;
                     const bool occ = (w[j] & W_OCC) != 0;
                     const ChargerResult r = charger_step<true, true, kNonneg>(p, PK ? (w[j] & ~W_STATIC) : w[j],
