@@ -1008,7 +1008,7 @@ int sng_create(const SngConfig *cfg, int device, int64_t num_envs, uint64_t seed
               alloc((void **)&ds.aux, tl * sizeof(double)) && alloc((void **)&ds.flags, E * sizeof(uint32_t)) &&
               alloc((void **)&ds.episode, sizeof(uint64_t)) && alloc((void **)&env->d_tables, sizeof(Tables));
     if (ok && p.req_enabled) ok = alloc((void **)&ds.req, tl * sizeof(double));
-    if (ok && p.noise) ok = alloc((void **)&ds.prof, 2 * (size_t)(T + 3) * E * sizeof(double));
+    if (ok && p.noise) ok = alloc((void **)&ds.prof_key, 2 * (size_t)E * sizeof(uint32_t));
     if (!ok) {
         std::string msg = g_create_error;
         sng_destroy(env);
@@ -1045,7 +1045,7 @@ void sng_destroy(SngEnv *env) {
         (void)hipEventDestroy(env->day_drawn);
     }
     DeviceState &ds = env->ds;
-    void *dev[] = {ds.soc, ds.bess, ds.bess0, ds.ratio, ds.pen0, ds.word, ds.aux, ds.req, ds.flags, ds.prof,
+    void *dev[] = {ds.soc, ds.bess, ds.bess0, ds.ratio, ds.pen0, ds.word, ds.aux, ds.req, ds.flags, ds.prof_key,
                    ds.episode, env->d_tables, env->rs.mt, env->rs.pos, env->ps.mt, env->ps.pos};
     for (void *x : dev)
         if (x) (void)hipFree(x);
@@ -1488,7 +1488,7 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 // Checkpoint / resume: header, then the sections in this order (host byte order):
 //   soc f64[N/2][E][2] (charger pairs) | bess, bess0, ratio, pen0 f64[E] | flags u32[E] | [word u32[T][N][E], host days]
 //   | aux 8B[T][N][E] (a packed day: its u32[T+1][N][E] records, sng_layout.h) | [req f64[T][N][E]]
-//   | [prof f64[2][T+3][E]] | [episode return f64[E]]
+//   | [profile keys u32[E][2]] | [episode return f64[E]]
 //   | [reference streams u32[E][2][625]]
 // ---------------------------------------------------------------------------------
 struct StateHeader {
@@ -1506,9 +1506,9 @@ struct StateHeader {
     uint64_t total_bytes;
 };
 // the last byte is the checkpoint format version: '3' since the configuration fingerprint is hashed
-// field by field (round 3), '4' since the SoC state is stored in charger pairs (round 4); a blob of another
-// version is refused as such
-static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '4'};
+// field by field (round 3), '5' since the SoC state is stored in charger pairs and a day's stochastic
+// profiles as per-env keys (round 4); a blob of another version is refused as such
+static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '5'};
 
 // The blob's size for this handle and the header's section flags.
 static uint64_t state_bytes(const SngEnv *env, const StateHeader &h) {
@@ -1516,7 +1516,7 @@ static uint64_t state_bytes(const SngEnv *env, const StateHeader &h) {
     size_t b = sizeof(StateHeader) + (size_t)env->p.n * E * 8 + 4 * E * 8 + E * 4 + tl * 8;
     if (h.has_word) b += tl * 4;
     if (h.has_req) b += tl * 8;
-    if (h.has_prof) b += 2 * (size_t)(env->p.T + 3) * E * 8;
+    if (h.has_prof) b += 2 * (size_t)E * 4;
     if (h.has_return) b += E * 8;
     if (h.has_streams) b += E * 2 * MT19937::kStateWords * 4;
     return b;
@@ -1546,7 +1546,7 @@ static StateHeader state_layout(const SngEnv *env, bool with_return) {
     h.replays = env->replays;
     h.has_word = env->p.packed ? 0 : 1;
     h.has_req = (env->ds.req && env->p.req_stream) ? 1 : 0;
-    h.has_prof = env->ds.prof ? 1 : 0;
+    h.has_prof = env->ds.prof_key ? 1 : 0;
     h.has_return = with_return ? 1 : 0;
     h.has_streams = env->py_seeded ? 1 : 0;
     h.total_bytes = state_bytes(env, h);
@@ -1599,7 +1599,7 @@ int sng_get_state(SngEnv *env, void *buf, size_t bytes, const double *episode_re
     if (h.has_word) HIP_TRY(env, pull(env->ds.word, tl * 4));
     HIP_TRY(env, pull(env->ds.aux, tl * 8));
     if (h.has_req) HIP_TRY(env, pull(env->ds.req, tl * 8));
-    if (h.has_prof) HIP_TRY(env, pull(env->ds.prof, 2 * (size_t)(env->p.T + 3) * E * 8));
+    if (h.has_prof) HIP_TRY(env, pull(env->ds.prof_key, 2 * (size_t)E * 4));
     if (h.has_return) HIP_TRY(env, pull(episode_return, E * 8));
     HIP_TRY(env, hipStreamSynchronize(st));
     if (h.has_streams) {
@@ -1645,7 +1645,7 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
     if (h.total_bytes > bytes) return fail(env, SNG_ERR_INVALID_ARGUMENT, "truncated state");
     if (h.has_return && !episode_return)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "the state holds day returns: pass an episode_return array");
-    if ((h.has_prof != 0) != (env->ds.prof != nullptr)) return fail(env, SNG_ERR_INVALID_ARGUMENT, "profile mismatch");
+    if ((h.has_prof != 0) != (env->ds.prof_key != nullptr)) return fail(env, SNG_ERR_INVALID_ARGUMENT, "profile mismatch");
     if (h.t < -1 || h.t > env->p.T) return fail(env, SNG_ERR_INVALID_ARGUMENT, "bad timestep in state");
     HIP_TRY(env, hipSetDevice(env->device));
     hipStream_t st = as_stream(stream);
@@ -1701,7 +1701,7 @@ int sng_set_state(SngEnv *env, const void *buf, size_t bytes, double *episode_re
     if (h.has_word) HIP_TRY(env, push(env->ds.word, tl * 4));
     HIP_TRY(env, push(env->ds.aux, tl * 8));
     if (h.has_req) HIP_TRY(env, push(env->ds.req, tl * 8));
-    if (h.has_prof) HIP_TRY(env, push(env->ds.prof, 2 * (size_t)(env->p.T + 3) * E * 8));
+    if (h.has_prof) HIP_TRY(env, push(env->ds.prof_key, 2 * (size_t)E * 4));
     if (h.has_return) HIP_TRY(env, push(episode_return, E * 8));
     if (h.has_streams) {
         HIP_TRY(env, hipMemcpy2DAsync(env->rs.mt, 2 * kMtN * sizeof(uint32_t), np_words.data(), kMtN * sizeof(uint32_t),

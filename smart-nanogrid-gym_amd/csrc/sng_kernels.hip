@@ -351,12 +351,28 @@ constexpr uint32_t kDomainPrice = 0x50520000u;
 
 // Build-defined stochastic profile factor 1 + sigma * z, z = h * 2^-31 - 1 in [-1, 1), of table
 // entry k for the env with seed env_seed on day `day` (SngConfig.pv_noise / price_noise).
-__device__ __forceinline__ double profile_factor(uint64_t env_seed, uint32_t domain, uint64_t day, int k,
-                                                 double sigma) {
-    const uint32_t key = stream_key(env_seed, 0, domain, day);
+// The same from the day's key of the env and domain, stream_key(env_seed, 0, domain, day): what a reset keeps
+// per env (DeviceState::prof_key) and the step kernels expand (round 4; round 3 stored every factor, 1.6 KB
+// per env and day at config 5, and loaded 64 B per env-step).  sigma = 0 gives 1.0 exactly.
+__device__ __forceinline__ double profile_factor_key(uint32_t key, int k, double sigma) {
+    if (sigma == 0.0) return 1.0;
     const uint32_t h = mix32(key + (uint32_t)k * 0x9e3779b9u);
     const double z = (double)h * 0x1.0p-31 - 1.0;
     return 1.0 + sigma * z;
+}
+__device__ __forceinline__ double profile_factor(uint64_t env_seed, uint32_t domain, uint64_t day, int k,
+                                                 double sigma) {
+    return profile_factor_key(stream_key(env_seed, 0, domain, day), k, sigma);
+}
+// The day's profile keys of an env (PV, price) from DeviceState::prof_key ([E][2] u32, one 8 B load).
+__device__ __forceinline__ void profile_factors(const Params &p, const DeviceState &s, uint32_t el8, int t,
+                                                double *fpv, double *fpr) {
+    const v2u kk = __builtin_bit_cast(v2u, bld(reinterpret_cast<const uint64_t *>(s.prof_key), el8));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        fpv[j] = profile_factor_key(kk.x, t + j, p.pv_noise);
+        fpr[j] = profile_factor_key(kk.y, t + j, p.price_noise);
+    }
 }
 
 // Per-step constants staged in LDS by the step kernel: irr_norm[t..t+3], price_norm[t..t+3],
@@ -1005,14 +1021,7 @@ struct WideGroup {
         ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
 #pragma unroll
         for (int j = 0; j < 4; ++j) fpv[j] = fpr[j] = 1.0;
-        if constexpr (NOISE) {   // the day's profile factors of t..t+3 (profile_kernel)
-            const size_t pp = (size_t)(p.T + 3) * E;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                fpv[j] = bld(s.prof + (size_t)(t + j) * E, el8);
-                fpr[j] = bld(s.prof + pp + (size_t)(t + j) * E, el8);
-            }
-        }
+        if constexpr (NOISE) profile_factors(p, s, el8, t, fpv, fpr);   // the day's profile factors of t..t+3
 #pragma unroll
         for (int j = 0; j < CPL; ++j) {
             // charger `charger(part, j)` (past a ragged lane's range: its charger NC - 1 again, discarded)
@@ -1426,14 +1435,7 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
     //    branches, ahead of the tile)
     load_req(cbeg);
     double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
-    if (p.noise) {
-        const size_t plane = (size_t)(p.T + 3) * E;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            fpv[j] = bld(s.prof + (size_t)(t + j) * E, el8);
-            fpr[j] = bld(s.prof + plane + (size_t)(t + j) * E, el8);
-        }
-    }
+    if (p.noise) profile_factors(p, s, el8, t, fpv, fpr);
     // 3. tables and the wave's actions tile
     //    (wide stations: no 1/c table, the step constants in scalar registers -- see StepLds)
     constexpr int RCP_PER_LANE = kRows ? 256 / kWave : 0;
@@ -1743,14 +1745,7 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
         // a generated day's python index -1 slot holds zeros; a replayed day's Requested_SOC is 0
         if (mode != OBS0_HOST) s.pen0[e] = 0.0;   // OBS0_GENERATED included
         double fpv[4] = {1.0, 1.0, 1.0, 1.0}, fpr[4] = {1.0, 1.0, 1.0, 1.0};
-        if (p.noise) {
-            const size_t plane = (size_t)(p.T + 3) * E;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                fpv[j] = s.prof[(size_t)j * E + e];
-                fpr[j] = s.prof[plane + (size_t)j * E + e];
-            }
-        }
+        if (p.noise) profile_factors(p, s, (uint32_t)e * 8u, 0, fpv, fpr);
         write_obs_header(o_row, p, s.tables->irr_norm, s.tables->price_norm, ratio, fpv, fpr);
         const int k = p.pv ? 8 : 4;
         const uint32_t *__restrict__ word = s.word;
@@ -1811,22 +1806,18 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
 }
 
 // ---------------------------------------------------------------------------------
-// Stochastic PV / price profiles of the day (build-defined, SngConfig.pv_noise / price_noise):
-// prof[0][k][e] = PV factor, prof[1][k][e] = price factor, k in [0, T + 3).  Runs in every reset
-// before observe0_kernel, which advances the day counter it reads.  Thread = env.
+// Stochastic PV / price profiles of the day (build-defined, SngConfig.pv_noise / price_noise): the env's
+// day keys prof_key[e] = {PV key, price key}, from which the step and observation kernels expand the factor
+// of entry k (profile_factor_key).  Runs in every reset before observe0_kernel, which advances the day
+// counter it reads.  Thread = env.
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void profile_kernel(Params p, DeviceState s, int64_t E) {
     const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (e >= E) return;
     const uint64_t day = *s.episode;
     const uint64_t env_seed = p.seed + (uint64_t)p.env_offset + (uint64_t)e;
-    const int K = p.T + 3;
-    const size_t plane = (size_t)K * E;
-    for (int k = 0; k < K; ++k) {
-        s.prof[(size_t)k * E + e] = p.pv_noise != 0.0 ? profile_factor(env_seed, kDomainPV, day, k, p.pv_noise) : 1.0;
-        s.prof[plane + (size_t)k * E + e] =
-            p.price_noise != 0.0 ? profile_factor(env_seed, kDomainPrice, day, k, p.price_noise) : 1.0;
-    }
+    s.prof_key[2 * e] = stream_key(env_seed, 0, kDomainPV, day);
+    s.prof_key[2 * e + 1] = stream_key(env_seed, 0, kDomainPrice, day);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1933,13 +1924,9 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
     if (le < nblk) {
         const uint64_t ge = (uint64_t)(e + p.env_offset);
         const uint64_t env_seed = p.seed + (uint64_t)p.env_offset + (uint64_t)e;
-        if (p.noise) {   // the day's profile factors prof[2][T + 3][E] (profile_kernel's), k = part mod 4
-            const size_t pl = (size_t)(p.T + 3) * E;
-            for (int k = part; k < p.T + 3; k += kObsParts) {
-                s.prof[(size_t)k * E + e] = p.pv_noise != 0.0 ? profile_factor(env_seed, kDomainPV, day, k, p.pv_noise) : 1.0;
-                s.prof[pl + (size_t)k * E + e] =
-                    p.price_noise != 0.0 ? profile_factor(env_seed, kDomainPrice, day, k, p.price_noise) : 1.0;
-            }
+        if (p.noise && part == 0) {   // the day's profile keys (profile_kernel's)
+            s.prof_key[2 * e] = stream_key(env_seed, 0, kDomainPV, day);
+            s.prof_key[2 * e + 1] = stream_key(env_seed, 0, kDomainPrice, day);
         }
         if (part == 0) {
             const double ratio = pv_ratio_draw(seed, ge, day);

@@ -115,7 +115,7 @@ struct Params {
     double grid_w, bat_pen_w, sell_coef;
     int64_t env_offset;       // global index of env 0 of this handle (sharded runs)
     int32_t lanes;            // step kernel: lanes per environment (1, 2 or 4)
-    int32_t noise;            // 1: stochastic PV / price profiles (DeviceState::prof is live)
+    int32_t noise;            // 1: stochastic PV / price profiles (DeviceState::prof_key is live)
     int32_t packed;           // 1: the day's timeline is packed records in `aux` (device-RNG days)
     int32_t req_zero;         // 1: Requested_SOC is 0 on every slot -- a replayed day: load_initial_values
                               //    (charging_station.py:119-136) does not restore what clear_initialisation_
@@ -166,8 +166,9 @@ struct DeviceState {
     uint32_t *word;
     double *aux, *req;
     uint32_t *flags;
-    // profile factors of the current day, [2][T + 3][E] (PV, price), only when Params::noise
-    double *prof;
+    // the current day's profile keys [E][2] (PV, price: stream_key of the env's seed and the day), only when
+    // Params::noise; the kernels expand factor k as profile_factor_key(key, k, sigma)
+    uint32_t *prof_key;
     uint64_t *episode;        // device-side day counter for the device generator
     const Tables *tables;
 };
