@@ -1337,12 +1337,12 @@ int sng_get_vehicle_soc(SngEnv *env, double *h, void *stream) {
     HIP_TRY(env, hipMemcpyAsync(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost, st));
     // a packed day: an empty charger's running SoC carries the next arrival's (sng_layout.h); SOC[c, t]
     // shows 0 there.  Occupancy of the last stepped step t - 1 is its record's OCC bit (plane t)
-    std::vector<uint32_t> rec;
+    std::vector<uint16_t> rec;
     const bool packed_mid = env->p.packed && env->t >= 1;
     if (packed_mid) {
         rec.resize((size_t)N * env->E);
-        HIP_TRY(env, hipMemcpyAsync(rec.data(), reinterpret_cast<const uint32_t *>(env->ds.aux) + (size_t)env->t * rec.size(),
-                                    rec.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipMemcpyAsync(rec.data(), reinterpret_cast<const uint16_t *>(env->ds.aux) + (size_t)env->t * rec.size(),
+                                    rec.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(env, hipStreamSynchronize(st));
     for (int64_t e = 0; e < env->E; ++e)
@@ -1361,13 +1361,13 @@ int sng_set_vehicle_soc(SngEnv *env, const double *h, void *stream) {
     std::vector<double> tmp((size_t)N * env->E);
     hipStream_t st = as_stream(stream);
     // a packed day mid-day: empty chargers keep the arrival SoC their running SoC carries (sng_layout.h)
-    std::vector<uint32_t> rec;
+    std::vector<uint16_t> rec;
     const bool packed_mid = env->p.packed && env->t >= 1;
     if (packed_mid) {
         rec.resize(tmp.size());
         HIP_TRY(env, hipMemcpyAsync(tmp.data(), env->ds.soc, tmp.size() * sizeof(double), hipMemcpyDeviceToHost, st));
-        HIP_TRY(env, hipMemcpyAsync(rec.data(), reinterpret_cast<const uint32_t *>(env->ds.aux) + (size_t)env->t * rec.size(),
-                                    rec.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipMemcpyAsync(rec.data(), reinterpret_cast<const uint16_t *>(env->ds.aux) + (size_t)env->t * rec.size(),
+                                    rec.size() * sizeof(uint16_t), hipMemcpyDeviceToHost, st));
         HIP_TRY(env, hipStreamSynchronize(st));
     }
     for (int64_t e = 0; e < env->E; ++e)
@@ -1400,12 +1400,12 @@ int sng_get_scenario(SngEnv *env, int64_t first, int64_t count, int32_t V, doubl
     const size_t rows = (size_t)T * N, pitch = (size_t)env->E, cnt = (size_t)count;
     std::vector<uint32_t> w(rows * cnt);
     std::vector<double> aux(rows * cnt), rq;
-    std::vector<uint32_t> rec;
-    if (env->p.packed) {   // device-RNG day: packed records in the aux buffer (sng_layout.h), T + 1 planes
+    std::vector<uint16_t> rec;
+    if (env->p.packed) {   // device-RNG day: 2 B packed records in the aux buffer (sng_layout.h), T + 1 planes
         rec.resize(rows * cnt + (size_t)N * cnt);
-        HIP_TRY(env, hipMemcpy2DAsync(rec.data(), cnt * sizeof(uint32_t),
-                                      reinterpret_cast<const uint32_t *>(env->ds.aux) + first, pitch * sizeof(uint32_t),
-                                      cnt * sizeof(uint32_t), rows + N, hipMemcpyDeviceToHost, st));
+        HIP_TRY(env, hipMemcpy2DAsync(rec.data(), cnt * sizeof(uint16_t),
+                                      reinterpret_cast<const uint16_t *>(env->ds.aux) + first, pitch * sizeof(uint16_t),
+                                      cnt * sizeof(uint16_t), rows + N, hipMemcpyDeviceToHost, st));
     } else {
         HIP_TRY(env, hipMemcpy2DAsync(w.data(), cnt * sizeof(uint32_t), env->ds.word + first, pitch * sizeof(uint32_t),
                                       cnt * sizeof(uint32_t), rows, hipMemcpyDeviceToHost, st));
@@ -1421,12 +1421,14 @@ int sng_get_scenario(SngEnv *env, int64_t first, int64_t count, int32_t V, doubl
     HIP_TRY(env, hipMemcpyAsync(pv_ratio, env->ds.ratio + first, cnt * sizeof(double), hipMemcpyDeviceToHost, st));
     HIP_TRY(env, hipStreamSynchronize(st));
     if (env->p.packed) {
-        // step t's record is plane t + 1; an arrival's SoC is carried by the record before it (plane t),
-        // and an empty charger shows 0
+        // step t's record is plane t + 1 (as a word: capacity and steps left in the word's fields); an
+        // arrival's SoC is carried by the record before it (plane t), and an empty charger shows 0
         const size_t plane = (size_t)N * cnt;
         for (size_t i = 0; i < rows * cnt; ++i) {
-            w[i] = rec[plane + i];
-            aux[i] = (w[i] & W_STATIC) ? (double)rec_soc(rec[i]) : 0.0;
+            const uint32_t r = rec[plane + i];
+            const bool occ = (r & W_OCC) != 0;
+            w[i] = occ ? pack_word(true, (r & W_STATIC) != 0, (r & W_PEN) != 0, rec_cap(r), rec_dep(r)) : (r & W_PEN);
+            aux[i] = (occ && (r & W_STATIC)) ? (double)rec_soc(rec[i]) : 0.0;
         }
     }
     for (size_t k = 0; k < cnt; ++k) {
@@ -1487,7 +1489,7 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 // ---------------------------------------------------------------------------------
 // Checkpoint / resume: header, then the sections in this order (host byte order):
 //   soc f64[N/2][E][2] (charger pairs) | bess, bess0, ratio, pen0 f64[E] | flags u32[E] | [word u32[T][N][E], host days]
-//   | aux 8B[T][N][E] (a packed day: its u32[T+1][N][E] records, sng_layout.h) | [req f64[T][N][E]]
+//   | aux 8B[T][N][E] (a packed day: its u16[T+1][N][E] records, sng_layout.h) | [req f64[T][N][E]]
 //   | [profile keys u32[E][2]] | [episode return f64[E]]
 //   | [reference streams u32[E][2][625]]
 // ---------------------------------------------------------------------------------
@@ -1506,8 +1508,8 @@ struct StateHeader {
     uint64_t total_bytes;
 };
 // the last byte is the checkpoint format version: '3' since the configuration fingerprint is hashed
-// field by field (round 3), '5' since the SoC state is stored in charger pairs and a day's stochastic
-// profiles as per-env keys (round 4); a blob of another version is refused as such
+// field by field (round 3), '5' since the SoC state is stored in charger pairs, a day's stochastic profiles
+// as per-env keys and a device day's records in 2 B (round 4); a blob of another version is refused as such
 static const char kStateMagic[8] = {'S', 'N', 'G', 'S', 'T', 'A', 'T', '5'};
 
 // The blob's size for this handle and the header's section flags.

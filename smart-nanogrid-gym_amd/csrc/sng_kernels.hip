@@ -167,6 +167,23 @@ __device__ __forceinline__ void bst(T *base, uint32_t voff, T v, uint32_t soff =
     else
         __builtin_amdgcn_raw_buffer_store_b8(__builtin_bit_cast(unsigned char, v), rsrc(base), voff, soff, POL);
 }
+// 2 B buffer accesses (the packed records of a device-RNG day, sng_layout.h), zero-extended.
+__device__ __forceinline__ uint32_t bld16(const uint16_t *base, uint32_t voff, uint32_t soff = 0) {
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(rsrc(base), voff, soff, 0);
+}
+template <int POL = 0>
+__device__ __forceinline__ void bst16(uint16_t *base, uint32_t voff, uint32_t v, uint32_t soff = 0) {
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)v, rsrc(base), voff, soff, POL);
+}
+// A device-RNG day's packed records (u16 [T+1][N][E] in the aux buffer) and a record's capacity field; a
+// host-RNG or injected day's word carries it in bits 8-15 (sng_layout.h).
+__device__ __forceinline__ const uint16_t *packed_records(const DeviceState &s) {
+    return reinterpret_cast<const uint16_t *>(s.aux);
+}
+template <bool PK>
+__device__ __forceinline__ uint32_t cap_field(uint32_t w) {
+    return PK ? (w >> P_CAP_SHIFT) & P_CAP_MASK : (w >> W_CAP_SHIFT) & 0xffu;
+}
 // Two f64 in one 16 B buffer access (a charger pair of the SoC state, sng_layout.h).
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 template <int POL = 0>
@@ -387,8 +404,9 @@ __host__ __device__ inline double step_constant(const Tables *tb, int t, int i) 
 // The reference rounds d / 24 in float64 and then to float32; for integers d < 256 that equals the
 // correctly rounded float32 quotient (d/24 is never a float32 rounding midpoint), which
 // q = d*r; q + fma(-q, 24, d)*r reproduces for every d < 256 (checked exhaustively).
+template <bool PK = false>   // PK: a packed record's steps-left field (bits 10-15; the record is zero-extended)
 __device__ __forceinline__ float departure_obs(uint32_t w) {
-    const float d = (float)((w >> W_DEP_SHIFT) & 0xffu);
+    const float d = PK ? (float)(w >> P_DEP_SHIFT) : (float)((w >> W_DEP_SHIFT) & 0xffu);
     constexpr float r24 = 1.0f / 24.0f;
     const float q = d * r24;
     return __builtin_fmaf(__builtin_fmaf(-q, 24.0f, d), r24, q);
@@ -428,7 +446,8 @@ struct ChargerResult {
 // takes only when none of its actions is negative, -0.0 or NaN.  Then a vehicle either charges (a > 0) or idles, so the discharge
 // branch -- the inverted-flag power (charger.py:122-132) and max(0, calc) -- is never selected and is not
 // computed; every value this returns equals the general form's for such actions.
-template <bool FAST, bool RCP, bool NONNEG = false>
+// PK: w is a device-RNG day's packed record (its capacity in bits 3-9), else a word.
+template <bool FAST, bool RCP, bool NONNEG = false, bool PK = false>
 __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, double req,
                                                       float a, int t, double rcap) {
     ChargerResult o;
@@ -449,7 +468,7 @@ __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t 
     const bool occ = (w & W_OCC) != 0;
     // previous SoC of an occupied charger, or the recorded SOC[c, t] of an empty one
     const double prev = (occ && !(w & W_STATIC)) ? run : aux;
-    const uint32_t capi = (w >> W_CAP_SHIFT) & 0xffu;
+    const uint32_t capi = cap_field<PK>(w);
     const double cap = (double)capi;
     const bool idle = (a == 0.0f);
     const bool chg = (a > 0.0f);
@@ -746,14 +765,14 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
     const double ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
     uint32_t w[NC];
     double aux[NC], run[NC], req[NC];
-    const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
+    const uint16_t *rec_t = packed_records(s) + plane + (size_t)NC * (size_t)E;   // t + 1
 #pragma unroll
     for (int c0 = 0; c0 < NC; c0 += 2) {   // charger pairs: the SoC state's 16 B slots (sng_layout.h)
 #pragma unroll
         for (int c = c0; c < c0 + 2 && c < NC; ++c) {
             const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
             if (PK) {   // packed device-day record (sng_layout.h): plane t + 1
-                w[c] = bld(rec_t, el4, r4);
+                w[c] = bld16(rec_t, el4 >> 1, r4 >> 1);
             } else {
                 w[c] = bld(s.word + plane, el4, r4);
                 aux[c] = bld(s.aux + plane, el8, r8);
@@ -792,19 +811,19 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
     if (live) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            const uint32_t capi = (w[c] >> W_CAP_SHIFT) & 0xffu;
+            const uint32_t capi = cap_field<PK>(w[c]);
             // a packed day: an arriving vehicle's SoC is the running SoC the step before stored (the
             // record it carried), so the step sees no STATIC bit and an empty charger's SoC is 0
             const bool occ = (w[c] & W_OCC) != 0;
-            const ChargerResult r = charger_step<true, true>(p, PK ? (w[c] & ~W_STATIC) : w[c], PK ? 0.0 : aux[c], run[c],
-                                                             req[c], av[c], t, recip_cap((double)capi));
+            const ChargerResult r = charger_step<true, true, false, PK>(p, PK ? (w[c] & ~W_STATIC) : w[c], PK ? 0.0 : aux[c],
+                                                                        run[c], req[c], av[c], t, recip_cap((double)capi));
             sv[c] = (PK && !occ) ? (double)rec_soc(w[c]) : r.soc;
             if (c & 1)   // the pair's 16 B slot once both chargers are stepped
                 bst2<kNT>(s.soc, 2u * el8, sv[c - 1], sv[c], (uint32_t)(c - 1) * (uint32_t)E * 8u);
             else if (c == NC - 1)
                 bst<kNT>(s.soc, el8, sv[c], (uint32_t)c * (uint32_t)E * 8u);
             o_row[k_soc + c] = (float)r.soc;
-            o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[c]);
+            o_row[k_soc + NC + c] = departure_obs<PK>((PK && !occ) ? 0u : w[c]);
             n_nonexist += r.nx;
             fl |= r.fl;
             pen_v += r.q;
@@ -1012,7 +1031,7 @@ struct WideGroup {
             row4_last = el4 + (uint32_t)(NC - 1) * (uint32_t)E * 4u;
         }
         const size_t plane = (size_t)t * NC * (size_t)E;   // this step's timeline planes
-        const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;   // t + 1
+        const uint16_t *rec_t = packed_records(s) + plane + (size_t)NC * (size_t)E;   // t + 1
         const int Ad = p.act_dim;
         act_tile.issue(act + e0 * Ad, nw * Ad, vec_io != 0, lane);
         ratio = bld(s.ratio, el8);
@@ -1026,8 +1045,8 @@ struct WideGroup {
         for (int j = 0; j < CPL; ++j) {
             // charger `charger(part, j)` (past a ragged lane's range: its charger NC - 1 again, discarded)
             const uint32_t v4 = row_of(j, nc, E), r4 = r4_of(j, E), v8 = 2u * v4, r8 = 2u * r4;
-            if (PK) {
-                w[j] = bld(rec_t, v4, r4);
+            if (PK) {   // a 2 B record: the 4 B plane offsets halved
+                w[j] = bld16(rec_t, v4 >> 1, r4 >> 1);
             } else {
                 w[j] = bld(s.word + plane, v4, r4);
                 aux[PK ? 0 : j] = bld(s.aux + plane, v8, r8);
@@ -1057,7 +1076,7 @@ struct WideGroup {
         const int c0 = part * CPL;
         const int nc = kPairs ? CPL : ((NC - c0) < CPL ? NC - c0 : CPL);
         const size_t plane = (size_t)t * NC * (size_t)E;
-        const uint32_t *rec_t = reinterpret_cast<const uint32_t *>(s.aux) + plane + (size_t)NC * (size_t)E;
+        const uint16_t *rec_t = packed_records(s) + plane + (size_t)NC * (size_t)E;
         const float *a_row = s_act + le * Ad;
         float *o_row = s_obs + le * O;
         float av[CPL];
@@ -1102,9 +1121,9 @@ struct WideGroup {
 #ifdef SNG_WIDE_PIN
                     asm volatile("" : "+v"(av[j]), "+v"(w[j]));   // A/B: pin the charger's inputs to its block
 #endif
-                    const uint32_t capi = (w[j] >> W_CAP_SHIFT) & 0xffu;
+                    const uint32_t capi = cap_field<PK>(w[j]);
                     const bool occ = (w[j] & W_OCC) != 0;
-                    const ChargerResult r = charger_step<true, true, kNonneg>(p, PK ? (w[j] & ~W_STATIC) : w[j],
+                    const ChargerResult r = charger_step<true, true, kNonneg, PK>(p, PK ? (w[j] & ~W_STATIC) : w[j],
                                                                            PK ? 0.0 : aux[PK ? 0 : j], run_[j], req_of(j, p),
                                                                            av[j], t, recip_cap((double)capi));
                     sv[j] = (PK && !occ) ? (double)rec_soc(w[j]) : r.soc;
@@ -1116,7 +1135,7 @@ struct WideGroup {
                         bst<kNT>(s.soc, (uint32_t)soc_index(c, el1, NC, E) * 8u, sv[j]);
                     }
                     o_row[k_soc + c] = (float)r.soc;
-                    o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : w[j]);
+                    o_row[k_soc + NC + c] = departure_obs<PK>((PK && !occ) ? 0u : w[j]);
                     n_nonexist += r.nx;
                     fl |= r.fl;
                     if (L > 1) qv[L > 1 ? j : 0] = r.q;
@@ -1177,7 +1196,7 @@ struct WideGroup {
                     pos.init();
 #pragma unroll 1
                     for (int c = 0; c < NC; ++c) {
-                        const uint32_t wc = PK ? bld(rec_t, el4, (uint32_t)c * (uint32_t)E * 4u)
+                        const uint32_t wc = PK ? bld16(rec_t, 2u * el1, (uint32_t)c * (uint32_t)E * 2u)
                                                : bld(s.word + plane, el4, (uint32_t)c * (uint32_t)E * 4u);
                         const float a = a_row[c];
                         const double pc = charging_power(p, a);
@@ -1197,17 +1216,17 @@ struct WideGroup {
                 for (int c = 0; c < NC; ++c) {
                     const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
                     const SocOff so = soc_off(c, NC, E, el8);
-                    const uint32_t wc = PK ? bld(rec_t, el4, r4) : bld(s.word + plane, el4, r4);
+                    const uint32_t wc = PK ? bld16(rec_t, 2u * el1, r4 >> 1) : bld(s.word + plane, el4, r4);
                     const double auxc = PK ? 0.0 : bld(s.aux + plane, el8, r8);
                     const double runc = bld(s.soc, so.v, so.s);
                     const double reqc = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
-                    const uint32_t capi = (wc >> W_CAP_SHIFT) & 0xffu;
+                    const uint32_t capi = cap_field<PK>(wc);
                     const bool occ = (wc & W_OCC) != 0;
-                    const ChargerResult r = charger_step<true, true>(p, PK ? (wc & ~W_STATIC) : wc, auxc, runc, reqc,
-                                                                     a_row[c], t, recip_cap((double)capi));
+                    const ChargerResult r = charger_step<true, true, false, PK>(p, PK ? (wc & ~W_STATIC) : wc, auxc, runc,
+                                                                                reqc, a_row[c], t, recip_cap((double)capi));
                     bst<kNT>(s.soc, so.v, (PK && !occ) ? (double)rec_soc(wc) : r.soc, so.s);
                     o_row[k_soc + c] = (float)r.soc;
-                    o_row[k_soc + NC + c] = departure_obs((PK && !occ) ? 0u : wc);
+                    o_row[k_soc + NC + c] = departure_obs<PK>((PK && !occ) ? 0u : wc);
                     n_nonexist += r.nx;
                     fl |= r.fl;
                     pen_v += r.q;
@@ -1347,7 +1366,7 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
     const uint32_t *__restrict__ word_t = word + tbase * (size_t)E;   // this step's timeline planes
     const double *__restrict__ aux_t = auxv + tbase * (size_t)E;
     // a packed day's records: plane t + 1 (sng_layout.h)
-    const uint32_t *__restrict__ rec_t = reinterpret_cast<const uint32_t *>(auxv) + (tbase + n) * (size_t)E;
+    const uint16_t *__restrict__ rec_t = packed_records(s) + (tbase + n) * (size_t)E;
     const double *__restrict__ req_t = reqv + tbase * (size_t)E;
     uint32_t w[CH];
     double aux[CH], run[CH], req[CH];
@@ -1358,7 +1377,7 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
             if (c < cend) {
                 const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
                 if (PK) {   // packed device-day record (sng_layout.h)
-                    w[j] = bld(rec_t, el4, r4);
+                    w[j] = bld16(rec_t, el4 >> 1, r4 >> 1);
                 } else {
                     w[j] = bld(word_t, el4, r4);
                     aux[j] = bld(aux_t, el8, r8);
@@ -1410,7 +1429,7 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
                 const int c = c0 + j;
                 const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
                 if (PK) {
-                    wn[j] = bld(rec_t, el4, r4);
+                    wn[j] = bld16(rec_t, el4 >> 1, r4 >> 1);
                 } else {
                     wn[j] = bld(word_t, el4, r4);
                     auxn[j] = bld(aux_t, el8, r8);
@@ -1534,18 +1553,18 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
                 // record, and reading every record's up front waited for all of them
                 // (wide stations: recip_cap instead of the LDS table, exact all the same -- div_by_cap)
 #ifdef SNG_X_WIDEDIV
-                rc[j] = kRows ? s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu] : 0.0;
+                rc[j] = kRows ? s_rcp[cap_field<PK>(w[j])] : 0.0;
 #else
-                rc[j] = kRows ? s_rcp[(w[j] >> W_CAP_SHIFT) & 0xffu] : recip_cap((double)((w[j] >> W_CAP_SHIFT) & 0xffu));
+                rc[j] = kRows ? s_rcp[cap_field<PK>(w[j])] : recip_cap((double)cap_field<PK>(w[j]));
 #endif
                 // a packed day: the arrival SoC is the running SoC the step before stored (sng_layout.h)
                 const bool occ = (w[j] & W_OCC) != 0;
                 const uint32_t wj = PK ? (w[j] & ~W_STATIC) : w[j];
                 const double aux_j = PK ? 0.0 : aux[j];
 #ifdef SNG_X_WIDEDIV
-                const ChargerResult r = charger_step<FAST, kRows>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
+                const ChargerResult r = charger_step<FAST, kRows, false, PK>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
 #else
-                const ChargerResult r = charger_step<FAST, true>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
+                const ChargerResult r = charger_step<FAST, true, false, PK>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
 #endif
                 const SocOff so = soc_off(c, n, E, el8);
                 bst<kNT>(socv, so.v, (PK && !occ) ? (double)rec_soc(w[j]) : r.soc, so.s);
@@ -1554,7 +1573,7 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
                     if (info.vehicle_soc) info.vehicle_soc[(size_t)e * n + c] = r.soc;
                 }
                 o_row[k_soc + c] = (float)r.soc;
-                o_row[k_soc + n + c] = departure_obs((PK && !occ) ? 0u : w[j]);
+                o_row[k_soc + n + c] = departure_obs<PK>((PK && !occ) ? 0u : w[j]);
                 n_nonexist += r.nx;
                 fl |= r.fl;
                 if (L == 1) {
@@ -1760,7 +1779,7 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
             double aux[B];
             if (PK) {   // packed device-day records (sng_layout.h): t = 0 is plane 1; plane 0 carries
                         // the SoC of the t = 0 arrivals
-                const uint32_t *rec = reinterpret_cast<const uint32_t *>(auxv);
+                const uint16_t *rec = packed_records(s);
                 uint32_t r0[B], r1[B];
 #pragma unroll
                 for (int j = 0; j < B; ++j) {
@@ -1791,7 +1810,7 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
                     else if (c + 1 == n && !(j & 1))
                         bst<kNT>(socv, (uint32_t)soc_index(c, e, n, E) * 8u, aux[j]);
                     o_row[k + c] = (float)aux[j];
-                    o_row[k + n + c] = departure_obs(w[j]);
+                    o_row[k + n + c] = departure_obs<PK>(w[j]);
                 }
             }
         }
@@ -1854,8 +1873,9 @@ __host__ __device__ constexpr size_t generate_lds_bytes(bool with_req) {
 struct VehicleDraw {
     int ta, dep;
     uint32_t cap;
-    double soc;
+    double soc;          // code_soc(code)
     uint32_t req_draw;
+    uint32_t code;       // the arrival SoC's 13-bit code (sng_layout.h)
 };
 __device__ __forceinline__ uint32_t mix32_gen(uint32_t x) {   // "lowbias32" (two multiplies, bijective)
     x ^= x >> 16;
@@ -1882,8 +1902,9 @@ __device__ __forceinline__ VehicleDraw draw_vehicle(const Params &p, GenStream &
     const uint32_t x1 = rng.next(), x2 = rng.next();
     const float u = ((float)(x1 >> 8) + 1.0f) * 0x1.0p-24f;   // (0, 1]
     d.ta = tfree + (int)(__log2f(u) * kInvLog2Q);               // floor: the product is >= 0
-    // uniform(0.1, 0.9) as a float32 value (the packed record holds it exactly): at most 0.9f
-    d.soc = (double)(0.1f + 0.8f * ((float)(x2 >> 8) * 0x1.0p-24f));
+    // uniform(0.1, 0.9) on 8,192 float32 values (the packed record holds the code, sng_layout.h code_soc)
+    d.code = x2 >> (32 - kSocCodeBits);
+    d.soc = (double)code_soc(d.code);
     const uint32_t r = ((x1 & 0xffu) << 8) | (x2 & 0xffu);
     const uint32_t rc = r * 105u;
     d.cap = p.diff_caps ? 15u + (rc >> 16) : 40u;   // randint(15, 120)
@@ -1990,11 +2011,13 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 #define SNG_GEN_POL kNT
 #endif
 constexpr int kGenRecPol = SNG_GEN_POL;
-// Vehicle list entries (LDS) are kept in the record's own layout: arrival step in bits 0-7 (the flag
-// bits of a record, masked off), capacity in 8-15 and departure step in 16-23, so an occupied step's
-// record is (entry & 0xffff00 | flags) - t << 16 (the departure field becomes the steps left; it is
-// > t while the vehicle is present, so nothing borrows); the arrival SoC is kept as the carry bits an
-// empty record holds (rec_carry), computed once per vehicle in phase 1.  TT: the day's step count as
+constexpr int kVehArrShift = 24;                   // vehicle list entry: arrival step (bits 24-31)
+constexpr uint32_t kVehRecMask = 0x3fff8u;         // capacity (3-9) and departure (10-17)
+// Vehicle list entries (LDS) are kept in the packed record's own layout: capacity in bits 3-9, departure
+// step in 10-17 and arrival step in 24-31, so an occupied step's record is (entry & 0x3fff8 | flags) -
+// t << 10 (the departure field becomes the steps left: it is > t while the vehicle is present, so nothing
+// borrows, and below 64, so bits 16-17 clear); the arrival SoC is kept as the carry bits an empty record
+// holds (rec_carry), computed once per vehicle in phase 1.  TT: the day's step count as
 // a compile-time constant (the walk unrolled: 24 for the 1 h day), 0 for a runtime p.T; REQ: the
 // requested-SoC stream.
 template <int TT, bool REQ>
@@ -2029,13 +2052,13 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     for (int v = 0; v < kDayVehicles - 1; ++v) {   // the last slot holds the sentinel
         if (tfree >= T) break;
 #ifdef SNG_GX_NOPH1
-        VehicleDraw d{tfree + 1, tfree + 7, 40u, 0.5, 0u};
+        VehicleDraw d{tfree + 1, tfree + 7, 40u, (double)code_soc(4096u), 0u, 4096u};
 #else
         const VehicleDraw d = draw_vehicle(p, rng, tfree, i4, i10, i1);
 #endif
         if (d.ta >= T) break;
-        s_veh[v * kGenBlock + tid] = (uint32_t)d.ta | (d.cap << W_CAP_SHIFT) | ((uint32_t)d.dep << W_DEP_SHIFT);
-        s_car[v * kGenBlock + tid] = rec_carry(false, (float)d.soc);   // a float32 value (draw_vehicle)
+        s_veh[v * kGenBlock + tid] = ((uint32_t)d.ta << kVehArrShift) | (d.cap << P_CAP_SHIFT) | ((uint32_t)d.dep << P_DEP_SHIFT);
+        s_car[v * kGenBlock + tid] = rec_carry(false, d.code);
         if (REQ) {
             const double lo = d.soc <= 0.9 ? d.soc + 0.1 : 1.0;
             s_req[v * kGenBlock + tid] = lo + (1.0 - lo) * u32_unit(d.req_draw);
@@ -2046,7 +2069,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
 
     // slot nv: a sentinel that never arrives or departs (arrival = departure = 255), so phase 2 walks
     // the list without a per-step bound check or branch (nv <= 7 < kDayVehicles, checked on the host)
-    s_veh[nv * kGenBlock + tid] = 0xffu | (0xffu << W_DEP_SHIFT);
+    s_veh[nv * kGenBlock + tid] = (0xffu << kVehArrShift) | (0xffu << P_DEP_SHIFT);
     s_car[nv * kGenBlock + tid] = 0u;
     if (REQ) s_req[nv * kGenBlock + tid] = 1.0;
 
@@ -2062,24 +2085,24 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     bool pen = false;   // step t is in the penalty-check list observe(t-1) built
     // step t occupied / its vehicle arriving at t, carried from step to step: step t + 1 is occupied iff
     // its vehicle arrives then (arr1) or step t's vehicle stays past t + 1
-    bool occ = (cur & 0xffu) == 0u, stat = occ;
+    bool occ = (cur >> kVehArrShift) == 0u, stat = occ;
     // penalty-check list built by observe(t-1) (charging_station.py:42-63) as one unsigned range
     // test on the steps the vehicle at t-1 had left: on_departure {1}, sparse {1..3}, dense any;
     // no_penalty never (lo = 256 > any remainder)
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
-    const uint32_t el4 = (uint32_t)e * 4u, el8 = (uint32_t)e * 8u;
-    const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
-    uint32_t *rec = reinterpret_cast<uint32_t *>(s.aux);
+    const uint32_t el2 = (uint32_t)e * 2u, el8 = (uint32_t)e * 8u;
+    const uint32_t r2 = (uint32_t)c * (uint32_t)E * 2u, r8 = 4u * r2;
+    uint16_t *rec = reinterpret_cast<uint16_t *>(s.aux);
     const size_t nE = (size_t)n * (size_t)E;
     // raw buffer stores: the plane in the V#, the charger row in soffset, the env in the lane offset
-    bst<kGenRecPol>(rec, el4, ((cur & 0xffu) == 0u) ? car_cur : 0u, r4);
+    bst16<kGenRecPol>(rec, el2, ((cur >> kVehArrShift) == 0u) ? car_cur : 0u, r2);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         // the vehicle of step t + 1: past the current departure, the next one (the list ends in a
         // sentinel that never arrives or departs)
-        const bool adv = (uint32_t)(t + 1) > (cur >> W_DEP_SHIFT);
+        const bool adv = (uint32_t)(t + 1) > ((cur >> P_DEP_SHIFT) & 0xffu);
         const uint32_t v1 = adv ? nxt : cur;
         const uint32_t car1 = adv ? car_nxt : car_cur;
         const double req1 = adv ? req_nxt : req_cur;
@@ -2089,22 +2112,24 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const double req_nxt1 = REQ ? s_req[nx] : 1.0;
 
         const uint32_t flags = W_OCC | (stat ? W_STATIC : 0u) | (pen ? W_PEN : 0u);
-        const uint32_t w_occ = ((cur & 0xffff00u) | flags) - ((uint32_t)t << W_DEP_SHIFT);   // dep -> dep - t
-        const bool arr1 = (v1 & 0xffu) == (uint32_t)(t + 1);   // step t + 1's vehicle arrives then
+        // capacity and departure in place, the departure becoming the steps left (dep > t while the vehicle
+        // is present, and dep - t <= 10 / dt < 64 fits the record's 6 bits: nothing borrows or spills)
+        const uint32_t w_occ = ((cur & kVehRecMask) | flags) - ((uint32_t)t << P_DEP_SHIFT);
+        const bool arr1 = (v1 >> kVehArrShift) == (uint32_t)(t + 1);   // step t + 1's vehicle arrives then
         const uint32_t carry = arr1 ? car1 : 0u;
         const uint32_t w_emp = (pen ? W_PEN : 0u) | carry;
 #ifdef SNG_GX_NOPH2
         if ((occ ? w_occ : w_emp) == 0xdeadbeefu)
 #endif
-        bst<kGenRecPol>(rec + (size_t)(t + 1) * nE, el4, occ ? w_occ : w_emp, r4);
+        bst16<kGenRecPol>(rec + (size_t)(t + 1) * nE, el2, occ ? w_occ : w_emp, r2);
         // requested SoC timeline (sng_layout.h): Requested_SOC[c, t-1] at t >= 1 -- the step reads
         // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
         if (REQ && t > 0) bst(s.req + (size_t)t * nE, el8, prev_occ ? req_cur : 0.0, r8);
         prev_occ = occ;
         // step t + 1's penalty check: occupied at t with dep - t steps left in [pen_lo, pen_lo + pen_span]
         // (w_occ's departure field holds dep - t; an empty charger is never in the list)
-        pen = occ && (w_occ >> W_DEP_SHIFT) - pen_lo <= pen_span;
-        occ = (occ && (uint32_t)(t + 1) < (cur >> W_DEP_SHIFT)) || arr1;
+        pen = occ && (w_occ >> P_DEP_SHIFT) - pen_lo <= pen_span;
+        occ = (occ && (uint32_t)(t + 1) < ((cur >> P_DEP_SHIFT) & 0xffu)) || arr1;
         stat = arr1;
         cur = v1;
         car_cur = car1;

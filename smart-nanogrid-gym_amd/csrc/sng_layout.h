@@ -15,18 +15,19 @@
 //   aux    f64 [T][N][E]    per charger-step static SoC: the "previous" SoC when the word's
 //                           STATIC bit is set (arrival: SOC[c, t] as generated), else the
 //                           SOC[c, t] an unoccupied charger shows
-//   rec    u32 [T+1][N][E]  device-RNG days only, in the aux buffer (`word` unused): one 4 B record
-//                           per charger-step instead of 12 B in two planes.  Plane t + 1 is step t's
-//                           record; plane 0 is a record "before the day".  An occupied charger's
-//                           record is its word (bits below).  An empty charger's record keeps OCC = 0
-//                           and PEN, and carries the arrival SoC of the vehicle that arrives at the
-//                           next step (REC_SOC, below; 0 when none): every arrival at t >= 1 follows an
-//                           empty step (the departure step stays empty, charging_station.py:239-251),
-//                           and plane 0 carries the t = 0 arrivals.  The step kernel stores the
-//                           carried SoC as an empty charger's running SoC, so the arrival step reads
-//                           it as the previous SoC; an empty charger shows 0 in the observation.  The
-//                           device generator draws its arrival SoC as a float32 value in [0.1, 0.9],
-//                           so the 25-bit field holds it exactly
+//   rec    u16 [T+1][N][E]  device-RNG days only, in the aux buffer (`word` unused): one 2 B record
+//                           per charger-step instead of 12 B in two planes (round 2: 4 B; round 4: 2 B).
+//                           Plane t + 1 is step t's record; plane 0 is a record "before the day".  An
+//                           occupied charger's record holds OCC, STATIC, PEN, the capacity and the steps
+//                           left (bits below).  An empty charger's record keeps OCC = 0 and PEN, and
+//                           carries the arrival SoC of the vehicle that arrives at the next step as a
+//                           13-bit code (0 when none): every arrival at t >= 1 follows an empty step (the
+//                           departure step stays empty, charging_station.py:239-251), and plane 0 carries
+//                           the t = 0 arrivals.  The step kernel stores the carried SoC as an empty
+//                           charger's running SoC, so the arrival step reads it as the previous SoC; an
+//                           empty charger shows 0 in the observation.  The device generator draws the
+//                           arrival SoC as one of 8,192 float32 values spread evenly over [0.1, 0.9]
+//                           (code_soc), so the code holds it exactly
 //   req    f64 [T][N][E]    Requested_SOC[c, t-1] (read by the penalty check where W_PEN is set);
 //                           the t = 0 slot, never read by a step, holds Requested_SOC[c, T-1] so the
 //                           day can be exported (sng_get_scenario); only when enabled
@@ -41,9 +42,9 @@
 //   bits 8-15  CAP     vehicle capacity in kWh used at step t (integer, 15..119 or 40)
 //   bits 16-23 DEP     departure time - t of the vehicle present at t (observation), 0 if none
 //
-// Packed record of an empty charger (OCC = 0): bit 2 PEN as above, bits 3-27 REC_SOC = the float32
-// bits of the next step's arrival SoC less 123 << 23 (a float in [2^-4, 1) has a biased exponent in
-// 123..126: 2 exponent bits + 23 mantissa bits), 0 when no vehicle arrives at the next step.
+// Packed record bits (u16, device-RNG days): bit 0 OCC, bit 1 STATIC, bit 2 PEN as in the word; occupied:
+// bits 3-9 CAP (7 bits: 15..119 or 40), bits 10-15 the steps left to departure (dep - t <= 10 / dt <= 53
+// for every dt of the 128-step timeline); empty: bits 3-15 the next step's arrival SoC code (code_soc).
 #pragma once
 #include <stdint.h>
 
@@ -78,15 +79,23 @@ SNG_HD inline size_t soc_index(int c, int64_t e, int n, int64_t E) {
     return (size_t)c0 * (size_t)E + (c0 + 2 <= n ? (size_t)e * 2u + (size_t)(c & 1) : (size_t)e);
 }
 
-constexpr int REC_SOC_SHIFT = 3;
-constexpr uint32_t kRecSocBias = 123u << 23;
-
-// An empty charger's packed record carrying arrival SoC `soc` (a float32 value in [2^-4, 1)).
-SNG_HD inline uint32_t rec_carry(bool pen, float soc) {
-    return (pen ? W_PEN : 0u) | ((__builtin_bit_cast(uint32_t, soc) - kRecSocBias) << REC_SOC_SHIFT);
+constexpr int P_CAP_SHIFT = 3, P_DEP_SHIFT = 10;   // packed record fields (above)
+constexpr uint32_t P_CAP_MASK = 0x7fu;
+constexpr int P_SOC_SHIFT = 3, kSocCodeBits = 13;
+// The arrival SoC of code k in [0, 8192): 0.1f + 0.8f * (k + 0.5) / 8192 in float32 (two roundings, no
+// contraction: the library builds with -ffp-contract=off), a value in (0.1, 0.9).
+SNG_HD inline float code_soc(uint32_t code) {
+    const float u = ((float)code + 0.5f) * (1.0f / 8192.0f);   // exact: code + 0.5 and the scaling by 2^-13
+    const float v = 0.8f * u;
+    return 0.1f + v;
 }
+// An empty charger's packed record carrying arrival SoC code `code`.
+SNG_HD inline uint32_t rec_carry(bool pen, uint32_t code) { return (pen ? W_PEN : 0u) | (code << P_SOC_SHIFT); }
 // The arrival SoC an empty charger's record carries (meaningful when the next step is an arrival).
-SNG_HD inline float rec_soc(uint32_t rec) { return __builtin_bit_cast(float, (rec >> REC_SOC_SHIFT) + kRecSocBias); }
+SNG_HD inline float rec_soc(uint32_t rec) { return code_soc((rec & 0xffffu) >> P_SOC_SHIFT); }
+// A packed record's capacity and steps left as the word's fields (host decode).
+SNG_HD inline uint32_t rec_cap(uint32_t rec) { return (rec >> P_CAP_SHIFT) & P_CAP_MASK; }
+SNG_HD inline uint32_t rec_dep(uint32_t rec) { return (rec & 0xffffu) >> P_DEP_SHIFT; }
 
 // Constant tables, in device memory, read with scalar (wave-uniform) loads.
 struct Tables {
