@@ -1347,8 +1347,8 @@ int sng_get_vehicle_soc(SngEnv *env, double *h, void *stream) {
     HIP_TRY(env, hipStreamSynchronize(st));
     for (int64_t e = 0; e < env->E; ++e)
         for (int c = 0; c < N; ++c) {
-            const size_t i = (size_t)c * env->E + e;   // the record plane; the SoC state is in charger pairs
-            h[e * N + c] = (packed_mid && !(rec[i] & W_OCC)) ? 0.0 : tmp[soc_index(c, e, N, env->E)];
+            // the record plane in charger quads, the SoC state in charger pairs (sng_layout.h)
+            h[e * N + c] = (packed_mid && !(rec[rec_index(c, e, N, env->E)] & W_OCC)) ? 0.0 : tmp[soc_index(c, e, N, env->E)];
         }
     return SNG_OK;
 }
@@ -1372,8 +1372,8 @@ int sng_set_vehicle_soc(SngEnv *env, const double *h, void *stream) {
     }
     for (int64_t e = 0; e < env->E; ++e)
         for (int c = 0; c < N; ++c) {
-            const size_t i = (size_t)c * env->E + e;   // the record plane; the SoC state is in charger pairs
-            if (!packed_mid || (rec[i] & W_OCC)) tmp[soc_index(c, e, N, env->E)] = h[e * N + c];
+            // the record plane in charger quads, the SoC state in charger pairs (sng_layout.h)
+            if (!packed_mid || (rec[rec_index(c, e, N, env->E)] & W_OCC)) tmp[soc_index(c, e, N, env->E)] = h[e * N + c];
         }
     HIP_TRY(env, hipMemcpyAsync(env->ds.soc, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice, st));
     HIP_TRY(env, hipStreamSynchronize(st));
@@ -1401,11 +1401,23 @@ int sng_get_scenario(SngEnv *env, int64_t first, int64_t count, int32_t V, doubl
     std::vector<uint32_t> w(rows * cnt);
     std::vector<double> aux(rows * cnt), rq;
     std::vector<uint16_t> rec;
-    if (env->p.packed) {   // device-RNG day: 2 B packed records in the aux buffer (sng_layout.h), T + 1 planes
+    if (env->p.packed) {   // device-RNG day: 2 B packed records in charger quads (sng_layout.h), T + 1 planes
+        // rec[plane][c][k] for the env range, one 2D copy (over the planes) per quad row: the range's slots
+        // of quad row c0 are one run of count * width records
         rec.resize(rows * cnt + (size_t)N * cnt);
-        HIP_TRY(env, hipMemcpy2DAsync(rec.data(), cnt * sizeof(uint16_t),
-                                      reinterpret_cast<const uint16_t *>(env->ds.aux) + first, pitch * sizeof(uint16_t),
-                                      cnt * sizeof(uint16_t), rows + N, hipMemcpyDeviceToHost, st));
+        std::vector<uint16_t> q((size_t)(T + 1) * 4 * cnt);
+        for (int c0 = 0; c0 < N; c0 += 4) {
+            const int wq = N - c0 < 4 ? N - c0 : 4;
+            HIP_TRY(env, hipMemcpy2DAsync(q.data(), cnt * wq * sizeof(uint16_t),
+                                          reinterpret_cast<const uint16_t *>(env->ds.aux) + (size_t)c0 * pitch + first * wq,
+                                          (size_t)N * pitch * sizeof(uint16_t), cnt * wq * sizeof(uint16_t), (size_t)T + 1,
+                                          hipMemcpyDeviceToHost, st));
+            HIP_TRY(env, hipStreamSynchronize(st));
+            for (int tp = 0; tp <= T; ++tp)
+                for (int cc = 0; cc < wq; ++cc)
+                    for (size_t k = 0; k < cnt; ++k)
+                        rec[((size_t)tp * N + c0 + cc) * cnt + k] = q[(size_t)tp * cnt * wq + k * wq + cc];
+        }
     } else {
         HIP_TRY(env, hipMemcpy2DAsync(w.data(), cnt * sizeof(uint32_t), env->ds.word + first, pitch * sizeof(uint32_t),
                                       cnt * sizeof(uint32_t), rows, hipMemcpyDeviceToHost, st));
@@ -1489,7 +1501,7 @@ int sng_get_tables(const SngEnv *env, double *irr, double *irr_max, double *pv_p
 // ---------------------------------------------------------------------------------
 // Checkpoint / resume: header, then the sections in this order (host byte order):
 //   soc f64[N/2][E][2] (charger pairs) | bess, bess0, ratio, pen0 f64[E] | flags u32[E] | [word u32[T][N][E], host days]
-//   | aux 8B[T][N][E] (a packed day: its u16[T+1][N][E] records, sng_layout.h) | [req f64[T][N][E]]
+//   | aux 8B[T][N][E] (a packed day: its u16 records in charger quads, sng_layout.h) | [req f64[T][N][E]]
 //   | [profile keys u32[E][2]] | [episode return f64[E]]
 //   | [reference streams u32[E][2][625]]
 // ---------------------------------------------------------------------------------

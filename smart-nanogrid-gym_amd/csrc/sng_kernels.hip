@@ -184,6 +184,23 @@ template <bool PK>
 __device__ __forceinline__ uint32_t cap_field(uint32_t w) {
     return PK ? (w >> P_CAP_SHIFT) & P_CAP_MASK : (w >> W_CAP_SHIFT) & 0xffu;
 }
+// Byte offset of charger c of env el in a packed-record plane (charger quads, sng_layout.h rec_index): the
+// per-lane part (v) and the wave-uniform quad row (s).
+struct RecOff {
+    uint32_t v, s;
+};
+__device__ __forceinline__ RecOff rec_off(int c, int n, int64_t E, uint32_t el) {
+    const int c0 = c & ~3;
+    const uint32_t w = (uint32_t)(n - c0 < 4 ? n - c0 : 4);
+    return {(el * w + (uint32_t)(c & 3)) * 2u, (uint32_t)c0 * (uint32_t)E * 2u};
+}
+// The four records of one 8 B quad slot.
+__device__ __forceinline__ void unpack_quad(uint64_t x, uint32_t *w) {
+    w[0] = (uint32_t)x & 0xffffu;
+    w[1] = (uint32_t)(x >> 16) & 0xffffu;
+    w[2] = (uint32_t)(x >> 32) & 0xffffu;
+    w[3] = (uint32_t)(x >> 48);
+}
 // Two f64 in one 16 B buffer access (a charger pair of the SoC state, sng_layout.h).
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 template <int POL = 0>
@@ -768,12 +785,21 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
     const uint16_t *rec_t = packed_records(s) + plane + (size_t)NC * (size_t)E;   // t + 1
 #pragma unroll
     for (int c0 = 0; c0 < NC; c0 += 2) {   // charger pairs: the SoC state's 16 B slots (sng_layout.h)
+        if (PK && (c0 & 3) == 0) {   // packed device-day records (sng_layout.h), plane t + 1: a quad per 8 B
+            if (c0 + 4 <= NC) {
+                unpack_quad(bld(reinterpret_cast<const uint64_t *>(rec_t), el1 * 8u, (uint32_t)c0 * (uint32_t)E * 2u), w + c0);
+            } else {
+#pragma unroll
+                for (int c = c0; c < NC; ++c) {
+                    const RecOff ro = rec_off(c, NC, E, el1);
+                    w[c] = bld16(rec_t, ro.v, ro.s);
+                }
+            }
+        }
 #pragma unroll
         for (int c = c0; c < c0 + 2 && c < NC; ++c) {
             const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
-            if (PK) {   // packed device-day record (sng_layout.h): plane t + 1
-                w[c] = bld16(rec_t, el4 >> 1, r4 >> 1);
-            } else {
+            if (!PK) {
                 w[c] = bld(s.word + plane, el4, r4);
                 aux[c] = bld(s.aux + plane, el8, r8);
             }
@@ -980,13 +1006,16 @@ struct WideGroup {
     static constexpr bool kNonneg = NC <= SNG_NONNEG_MAX;
     static constexpr int H = (NC - 2) / 2;
     static_assert(!kPairs || CPL == H + 1, "a lane's chargers: H from whole pairs and one from the last");
+    // the lane's whole pairs are whole record quads too (H a multiple of 4: N = 10, 50), and the last pair is
+    // the partial quad's two records
+    static constexpr bool kQuads = kPairs && H % 4 == 0;
     static __device__ __forceinline__ int charger(int part, int j) {
         return kPairs ? (j < H ? part * H + j : NC - 2 + part) : part * CPL + j;
     }
     int64_t e0;
     int nw;
     bool live;
-    uint32_t el1, el4, el8, row4, row4_last, soc_a, soc_b;
+    uint32_t el1, el4, el8, row4, row4_last, soc_a, soc_b, rec_a, rec_b;
     TileStage<KT, kWave> act_tile;
     double ratio, bess_l, pen0_l, ret_l;
     double fpv[4], fpr[4];
@@ -1023,6 +1052,8 @@ struct WideGroup {
             row4_last = el4 + (uint32_t)part * (uint32_t)E * 4u;      // charger N - 2 + part: + (N - 2) E (uniform)
             soc_a = 2u * el8 + (uint32_t)(part * H) * (uint32_t)E * 8u;   // pair row part H + j: + j E 8 (uniform)
             soc_b = 2u * el8 + (uint32_t)part * 8u;                      // the last pair's row: + (N - 2) E 8
+            rec_a = el1 * 8u + (uint32_t)(part * H) * (uint32_t)E * 2u;   // quad row part H + j: + j E 2 (uniform)
+            rec_b = el1 * 4u + (uint32_t)part * 2u;                      // the partial quad (N - 2, N - 1): + (N - 2) E 2
         } else {
             // the lane's first charger row as a per-lane byte offset; charger j of the lane adds j * E
             // (uniform).  Past the lane's range (j >= nc) the loads re-read its first charger and nothing is
@@ -1045,8 +1076,17 @@ struct WideGroup {
         for (int j = 0; j < CPL; ++j) {
             // charger `charger(part, j)` (past a ragged lane's range: its charger NC - 1 again, discarded)
             const uint32_t v4 = row_of(j, nc, E), r4 = r4_of(j, E), v8 = 2u * v4, r8 = 2u * r4;
-            if (PK) {   // a 2 B record: the 4 B plane offsets halved
-                w[j] = bld16(rec_t, v4 >> 1, r4 >> 1);
+            if (PK) {   // 2 B records in charger quads: the lane's whole quads as 8 B, its last-pair charger as 2 B
+                if constexpr (kQuads) {
+                    if (j < H && (j & 3) == 0)
+                        unpack_quad(bld(reinterpret_cast<const uint64_t *>(rec_t), rec_a, (uint32_t)j * (uint32_t)E * 2u),
+                                    w + j);
+                    if (j == H) w[j] = bld16(rec_t, rec_b, (uint32_t)(NC - 2) * (uint32_t)E * 2u);
+                } else {
+                    const int cr = charger(part, j) < NC ? charger(part, j) : NC - 1;
+                    const RecOff ro = rec_off(cr, NC, E, el1);
+                    w[j] = bld16(rec_t, ro.v, ro.s);
+                }
             } else {
                 w[j] = bld(s.word + plane, v4, r4);
                 aux[PK ? 0 : j] = bld(s.aux + plane, v8, r8);
@@ -1196,7 +1236,8 @@ struct WideGroup {
                     pos.init();
 #pragma unroll 1
                     for (int c = 0; c < NC; ++c) {
-                        const uint32_t wc = PK ? bld16(rec_t, 2u * el1, (uint32_t)c * (uint32_t)E * 2u)
+                        const RecOff ro = rec_off(c, NC, E, el1);
+                        const uint32_t wc = PK ? bld16(rec_t, ro.v, ro.s)
                                                : bld(s.word + plane, el4, (uint32_t)c * (uint32_t)E * 4u);
                         const float a = a_row[c];
                         const double pc = charging_power(p, a);
@@ -1216,7 +1257,8 @@ struct WideGroup {
                 for (int c = 0; c < NC; ++c) {
                     const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
                     const SocOff so = soc_off(c, NC, E, el8);
-                    const uint32_t wc = PK ? bld16(rec_t, 2u * el1, r4 >> 1) : bld(s.word + plane, el4, r4);
+                    const RecOff ro = rec_off(c, NC, E, el1);
+                    const uint32_t wc = PK ? bld16(rec_t, ro.v, ro.s) : bld(s.word + plane, el4, r4);
                     const double auxc = PK ? 0.0 : bld(s.aux + plane, el8, r8);
                     const double runc = bld(s.soc, so.v, so.s);
                     const double reqc = REQ ? bld(s.req + plane, el8, r8) : (p.req_zero ? 0.0 : 1.0);
@@ -1377,7 +1419,8 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
             if (c < cend) {
                 const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
                 if (PK) {   // packed device-day record (sng_layout.h)
-                    w[j] = bld16(rec_t, el4 >> 1, r4 >> 1);
+                    const RecOff ro = rec_off(c, n, E, el1);
+                    w[j] = bld16(rec_t, ro.v, ro.s);
                 } else {
                     w[j] = bld(word_t, el4, r4);
                     aux[j] = bld(aux_t, el8, r8);
@@ -1429,7 +1472,8 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
                 const int c = c0 + j;
                 const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;   // charger row
                 if (PK) {
-                    wn[j] = bld16(rec_t, el4 >> 1, r4 >> 1);
+                    const RecOff ro = rec_off(c, n, E, el1);
+                    wn[j] = bld16(rec_t, ro.v, ro.s);
                 } else {
                     wn[j] = bld(word_t, el4, r4);
                     auxn[j] = bld(aux_t, el8, r8);
@@ -1784,8 +1828,9 @@ __global__ __launch_bounds__(BLOCK) void observe0_kernel(Params p, DeviceState s
 #pragma unroll
                 for (int j = 0; j < B; ++j) {
                     const int c = c0 + j < n ? c0 + j : n - 1;
-                    r1[j] = rec[((size_t)n + c) * E + e];
-                    r0[j] = rec[(size_t)c * E + e];
+                    const size_t ri = rec_index(c, e, n, E);   // charger quads (sng_layout.h)
+                    r1[j] = rec[(size_t)n * E + ri];
+                    r0[j] = rec[ri];
                 }
 #pragma unroll
                 for (int j = 0; j < B; ++j) {
@@ -2011,6 +2056,8 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 #define SNG_GEN_POL kNT
 #endif
 constexpr int kGenRecPol = SNG_GEN_POL;
+// Timeline rows of the generator's grid: four 64-env rows per charger quad (see generate_kernel).
+__host__ __device__ constexpr int gen_rows(int n) { return 4 * ((n + 3) / 4); }
 constexpr int kVehArrShift = 24;                   // vehicle list entry: arrival step (bits 24-31)
 constexpr uint32_t kVehRecMask = 0x3fff8u;         // capacity (3-9) and departure (10-17)
 // Vehicle list entries (LDS) are kept in the packed record's own layout: capacity in bits 3-9, departure
@@ -2029,19 +2076,25 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     uint32_t *s_car = s_veh + kDaySlots * kGenBlock;                           // [V][BLOCK] arrival SoC carry bits
     double *s_req = reinterpret_cast<double *>(s_car + kDaySlots * kGenBlock);     // [V][BLOCK] (REQ only)
     const int tid = threadIdx.x;
-    const int64_t e = (int64_t)blockIdx.x * kGenBlock + tid;
-    // grid rows: the t = 0 observation blocks first (gridDim.y - N of them: dispatched first, their
-    // dependent table and BESS loads do not trail the timeline blocks), then charger c = y - rows
-    const int obs_rows = (int)gridDim.y - p.n;
-    const int c = (int)blockIdx.y - obs_rows;
+    // grid rows: the t = 0 observation blocks first (gridDim.y - gen_rows(N) of them: dispatched first,
+    // their dependent table and BESS loads do not trail the timeline blocks), then the timeline: row u
+    // of charger quad u / 4 and 64 envs [256 x + 64 (u mod 4), +64), thread = (env tid / 4, charger tid mod 4
+    // of the quad), so a wavefront's record stores are 16 envs x the quad's records, contiguous in the
+    // quad layout (sng_layout.h rec_index)
+    const int obs_rows = (int)gridDim.y - gen_rows(p.n);
+    const int u = (int)blockIdx.y - obs_rows;
     const uint64_t day = *s.episode;
-    if (c < 0) {
+    if (u < 0) {
 #ifndef SNG_GX_NOOBS   // diagnostic builds (tools/gpu_session.sh ablib) only: generator cost breakdown
         observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds, (int)blockIdx.y);
 #endif
         return;
     }
-    if (e >= E) return;
+    const int q4 = (u >> 2) * 4;                                // the quad's first charger
+    const int qw = p.n - q4 < 4 ? p.n - q4 : 4;                 // its width (the last quad may be partial)
+    const int c = q4 + (tid & 3);
+    const int64_t e = (int64_t)blockIdx.x * kGenBlock + (int64_t)(u & 3) * 64 + (tid >> 2);
+    if (e >= E || c >= p.n) return;
     const uint64_t ge = (uint64_t)(e + p.env_offset);   // global env id
     GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
     const int T = TT > 0 ? TT : p.T;
@@ -2092,11 +2145,14 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
-    const uint32_t el2 = (uint32_t)e * 2u, el8 = (uint32_t)e * 8u;
-    const uint32_t r2 = (uint32_t)c * (uint32_t)E * 2u, r8 = 4u * r2;
+    // the record slot (quad layout: the quad row in soffset, env and charger in the lane offset) and the
+    // requested-SoC slot ([N][E] planes: charger row and env in the lane offset)
+    const uint32_t el2 = ((uint32_t)e * (uint32_t)qw + (uint32_t)(c - q4)) * 2u;
+    const uint32_t r2 = (uint32_t)q4 * (uint32_t)E * 2u;
+    const uint32_t el8 = ((uint32_t)c * (uint32_t)E + (uint32_t)e) * 8u;
     uint16_t *rec = reinterpret_cast<uint16_t *>(s.aux);
     const size_t nE = (size_t)n * (size_t)E;
-    // raw buffer stores: the plane in the V#, the charger row in soffset, the env in the lane offset
+    // raw buffer stores: the plane in the V#, the quad row in soffset, the slot in the lane offset
     bst16<kGenRecPol>(rec, el2, ((cur >> kVehArrShift) == 0u) ? car_cur : 0u, r2);
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -2124,7 +2180,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         bst16<kGenRecPol>(rec + (size_t)(t + 1) * nE, el2, occ ? w_occ : w_emp, r2);
         // requested SoC timeline (sng_layout.h): Requested_SOC[c, t-1] at t >= 1 -- the step reads
         // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
-        if (REQ && t > 0) bst(s.req + (size_t)t * nE, el8, prev_occ ? req_cur : 0.0, r8);
+        if (REQ && t > 0) bst(s.req + (size_t)t * nE, el8, prev_occ ? req_cur : 0.0);
         prev_occ = occ;
         // step t + 1's penalty check: occupied at t with dep - t steps left in [pen_lo, pen_lo + pen_span]
         // (w_occ's departure field holds dep - t; an empty charger is never in the list)
@@ -2138,7 +2194,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         car_nxt = car_nxt1;
         req_nxt = req_nxt1;
     }
-    if (REQ) bst(s.req, el8, prev_occ ? req_cur : 0.0, r8);
+    if (REQ) bst(s.req, el8, prev_occ ? req_cur : 0.0);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2463,7 +2519,7 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
 #define SNG_GX_FUSE_MAX (32 * 1024)
 #endif
     const bool fused = tile <= SNG_GX_FUSE_MAX;   // up to 60 chargers (config 5's 50: 27.9 KB)
-    const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(p.n + (fused ? kObsBlocks : 0))),
+    const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(gen_rows(p.n) + (fused ? kObsBlocks : 0))),
         block(kGenBlock);
 #ifdef SNG_GX_SMALL_LDS   // diagnostic builds only (with SNG_GX_NOOBS): the list's LDS alone
     const size_t lds = veh;

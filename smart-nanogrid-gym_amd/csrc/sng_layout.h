@@ -15,8 +15,11 @@
 //   aux    f64 [T][N][E]    per charger-step static SoC: the "previous" SoC when the word's
 //                           STATIC bit is set (arrival: SOC[c, t] as generated), else the
 //                           SOC[c, t] an unoccupied charger shows
-//   rec    u16 [T+1][N][E]  device-RNG days only, in the aux buffer (`word` unused): one 2 B record
-//                           per charger-step instead of 12 B in two planes (round 2: 4 B; round 4: 2 B).
+//   rec    u16 [T+1][N/4][E][4]  device-RNG days only, in the aux buffer (`word` unused): one 2 B record
+//                           per charger-step instead of 12 B in two planes (round 2: 4 B; round 4: 2 B),
+//                           in charger quads: chargers 4k..4k+3 of env e are the 8 B at quad row k, slot
+//                           e (a last partial quad of R = N mod 4 chargers: slots of 2R B; rec_index), so
+//                           a lane reads four of its env's records in one 8 B load.
 //                           Plane t + 1 is step t's record; plane 0 is a record "before the day".  An
 //                           occupied charger's record holds OCC, STATIC, PEN, the capacity and the steps
 //                           left (bits below).  An empty charger's record keeps OCC = 0 and PEN, and
@@ -77,6 +80,13 @@ SNG_HD inline uint32_t pack_word(bool occ, bool stat, bool pen, uint32_t cap, ui
 SNG_HD inline size_t soc_index(int c, int64_t e, int n, int64_t E) {
     const int c0 = c & ~1;
     return (size_t)c0 * (size_t)E + (c0 + 2 <= n ? (size_t)e * 2u + (size_t)(c & 1) : (size_t)e);
+}
+
+// Element index of charger c, env e in a packed-record plane (charger quads, above).
+SNG_HD inline size_t rec_index(int c, int64_t e, int n, int64_t E) {
+    const int c0 = c & ~3;
+    const int w = n - c0 < 4 ? n - c0 : 4;
+    return (size_t)c0 * (size_t)E + (size_t)e * (size_t)w + (size_t)(c & 3);
 }
 
 constexpr int P_CAP_SHIFT = 3, P_DEP_SHIFT = 10;   // packed record fields (above)
