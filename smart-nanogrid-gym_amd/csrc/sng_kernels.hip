@@ -2056,8 +2056,11 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 #define SNG_GEN_POL kNT
 #endif
 constexpr int kGenRecPol = SNG_GEN_POL;
-// Timeline rows of the generator's grid: four 64-env rows per charger quad (see generate_kernel).
-__host__ __device__ constexpr int gen_rows(int n) { return 4 * ((n + 3) / 4); }
+// Timeline rows of the generator's grid (see generate_kernel): four rows of 64 envs per full charger quad; a
+// last partial quad of w = N mod 4 chargers has 256 / w envs per row (w = 1, 2: one or two rows), or 64 envs
+// with one lane in four idle (w = 3: four rows).
+__host__ __device__ constexpr int gen_part_lanes(int w) { return w == 3 ? 4 : w; }   // lanes per env
+__host__ __device__ constexpr int gen_rows(int n) { return 4 * (n / 4) + (n % 4 == 0 ? 0 : 4 * gen_part_lanes(n % 4) / 4); }
 constexpr int kVehArrShift = 24;                   // vehicle list entry: arrival step (bits 24-31)
 constexpr uint32_t kVehRecMask = 0x3fff8u;         // capacity (3-9) and departure (10-17)
 // Vehicle list entries (LDS) are kept in the packed record's own layout: capacity in bits 3-9, departure
@@ -2090,10 +2093,13 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
 #endif
         return;
     }
-    const int q4 = (u >> 2) * 4;                                // the quad's first charger
+    const int full = 4 * (p.n / 4);                              // timeline rows of the full quads
+    const int q4 = u < full ? (u >> 2) * 4 : p.n & ~3;          // the quad's first charger
     const int qw = p.n - q4 < 4 ? p.n - q4 : 4;                 // its width (the last quad may be partial)
-    const int c = q4 + (tid & 3);
-    const int64_t e = (int64_t)blockIdx.x * kGenBlock + (int64_t)(u & 3) * 64 + (tid >> 2);
+    const int lpe = u < full ? 4 : gen_part_lanes(qw);          // lanes per env: 256 / lpe envs per row
+    const int sub = u < full ? (u & 3) : u - full;              // the row's env block within the 256
+    const int c = q4 + tid % lpe;
+    const int64_t e = (int64_t)blockIdx.x * kGenBlock + (int64_t)sub * (kGenBlock / lpe) + tid / lpe;
     if (e >= E || c >= p.n) return;
     const uint64_t ge = (uint64_t)(e + p.env_offset);   // global env id
     GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
