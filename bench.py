@@ -59,13 +59,13 @@ def survey_bytes(n):
 
 def step_kernel_bytes(n, noise=False, flags=False):
     """What this layout moves per env-step of a device-RNG day (b-pv, no requested-SoC stream), as
-    (read, written): reads = actions 4(N+1) + packed 4-byte charger-step record 4N (sng_layout.h) + EV SoC
-    8N + BESS 8 + PV ratio 8 + day return 8 (+ 64 for the PV / price profile factors of t..t+3 with
-    stochastic profiles); writes = obs 4(2N+9) + reward 8 + done 1 + EV SoC 8N + BESS 8 + day return 8
-    (+ 4 for the per-env per-step error flags, flags=True: the diagnostics' SngInfo.flags; the default
-    SngInfo watches the one-word flag summary instead).  32N + 89 (+4) in all.  Host-RNG days
-    read the word and a float64 static SoC instead: 40N + 89."""
-    rd = 4 * (n + 1) + 4 * n + 8 * n + 8 + 8 + 8 + (64 if noise else 0)
+    (read, written): reads = actions 4(N+1) + packed 2-byte charger-step record 2N (round 4; sng_layout.h)
+    + EV SoC 8N + BESS 8 + PV ratio 8 + day return 8 (+ 8 for the env's two stochastic-profile keys);
+    writes = obs 4(2N+9) + reward 8 + done 1 + EV SoC 8N + BESS 8 + day return 8 (+ 4 for the per-env
+    per-step error flags, flags=True: the diagnostics' SngInfo.flags; the default SngInfo watches the
+    one-word flag summary instead).  30N + 89 (+4) in all.  Host-RNG days read the word and a float64
+    static SoC instead: 40N + 89."""
+    rd = 4 * (n + 1) + 2 * n + 8 * n + 8 + 8 + 8 + (8 if noise else 0)
     wr = 4 * (2 * n + 9) + 8 + 1 + 8 * n + 8 + 8 + (4 if flags else 0)
     return rd, wr
 
