@@ -21,6 +21,7 @@ Reference behaviour mirrored per env (smart_nanogrid_gym/envs/smart_nanogrid_env
   errors   -> the reference's ValueErrors, raised after the step that hit them
 """
 import ctypes
+import itertools
 import time
 import warnings
 
@@ -42,6 +43,12 @@ except Exception:
     _VecEnvBase = object
 
 SLOTS = 25
+
+
+def _empty_infos(n):
+    """n distinct empty dicts (SB3's per-env infos): dict() mapped over a repeat runs in C, about a quarter
+    faster than a list comprehension of {} at 65,536 envs."""
+    return list(itertools.starmap(dict, itertools.repeat((), n)))
 
 
 def _stream_handle(device):
@@ -369,7 +376,7 @@ class SmartNanogridVecEnv(_VecEnvBase):
                 t1 = time.perf_counter()
             # the per-env info dicts SB3 expects (one fresh dict per env) are built while the device works
             last = lib().sng_get_timestep(self._h) + 1 >= self.timesteps
-            infos = None if last else [{} for _ in range(E)]
+            infos = None if last else _empty_infos(E)
             stream.synchronize()
         if prof is not None:
             t2 = time.perf_counter()
@@ -384,7 +391,7 @@ class SmartNanogridVecEnv(_VecEnvBase):
             # wait for the caller's next reset()
             infos = [{"terminal_observation": o, "TimeLimit.truncated": False} for o in obs]
         elif infos is None:
-            infos = [{} for _ in range(E)]
+            infos = _empty_infos(E)
         if flags is not None:
             for i in np.nonzero(flags & _native.FLAG_V2X_BREAKPOINT)[0]:
                 infos[i]["v2x_breakpoint"] = True
