@@ -155,8 +155,8 @@ def rocprof_average_us(kernel, extended):
     """Average duration (us) of `kernel` in the newest committed rocprofv3 --stats summary of this
     configuration (profiles/rNN_kernel_stats[_config5].csv), with the file it came from."""
     pat = "r*_kernel_stats_config5.csv" if extended else "r*_kernel_stats.csv"
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)),
-                   key=lambda f: int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)),   # by round, then name (deterministic)
+                   key=lambda f: (int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)), os.path.basename(f)))
     for path in reversed(files):
         with open(path) as fp:
             for line in fp:
