@@ -8,8 +8,13 @@ stream, overlapped with the next replay's kernels.  Actions are synthetic (unifo
 action Box, 20 % exact zeros), pre-generated on the device outside the timed region.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs E] [--chargers C] [--no-cpu-baseline]
+        # N > 1: this process measures cpu_baseline, then starts N rank processes itself
+        # (torch.distributed.run as a child process) and exits with their status
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
         [--dist-backend gloo]   # several ranks on one GPU: day returns gathered through host memory
+    A launcher's WORLD_SIZE that differs from --gpus is refused (exit 2), as is --gpus N > 1 with RCCL
+    and fewer than N visible GPUs.  The line's `dist` object reports the process group's backend and the
+    world size it initialised.
 
 Rank 0 prints one JSON line.  `roofline` describes the dominant kernel (the fused step):
 achieved = SURVEY.md 8(d)'s algorithmic bytes per env-step, B(N) = 40 N + 65 (465 B at N = 10),
@@ -199,6 +204,40 @@ def copy_ceiling(device, read_bytes, write_bytes, reps=50):
             "gbs_back_to_back": round(tot / (b_us.value * 1e-6) / 1e9, 1)}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, kw):
+    """`bench.py --gpus N` (N > 1) without a launcher: measure the CPU baseline here, before anything
+    touches the GPU, then start N fresh rank processes with torch.distributed.run (a child process, never
+    an exec of this one) and return its exit code.  Rank 0 prints the JSON line with this process's
+    cpu_baseline (handed over in a file named by SNG_BENCH_CPU_BASELINE)."""
+    import subprocess
+    import tempfile
+    ndev = torch.cuda.device_count()   # does not initialise the GPU on this image
+    if args.dist_backend == "nccl" and ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL (one rank per GPU); "
+              f"{ndev} visible (--dist-backend gloo shares them)", file=sys.stderr)
+        return 2
+    cpu = None if args.no_cpu_baseline else cpu_baseline(kw, args.cpu_budget)
+    with tempfile.NamedTemporaryFile("w", suffix=".json", prefix="sng_cpu_baseline_", delete=False) as fp:
+        json.dump(cpu, fp)
+        cpu_file = fp.name
+    env = dict(os.environ, SNG_BENCH_CPU_BASELINE=cpu_file, SNG_BENCH_LAUNCHER="bench.py --gpus (torch.distributed.run child)")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    try:
+        return subprocess.run(cmd, env=env).returncode
+    finally:
+        os.unlink(cpu_file)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -224,9 +263,6 @@ def main():
                          "SngInfo watches the flag summary word instead)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     E, N = args.envs, args.chargers
     kw = dict(number_of_chargers=N, time_interval=args.time_interval, charging_mode="bounded",
               vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
@@ -234,14 +270,36 @@ def main():
     noise = args.pv_noise > 0 or args.price_noise > 0
     if args.extended_day or noise:
         kw.update(extended_day=args.extended_day, pv_noise=args.pv_noise, price_noise=args.price_noise)
-    # the CPU baseline is a rank-0, single-GPU report, measured before the GPU is initialised (forked
-    # workers, host cores otherwise idle)
-    cpu = None if (args.no_cpu_baseline or world > 1) else cpu_baseline(kw, args.cpu_budget)
+    if args.gpus < 1:
+        print(f"bench.py: --gpus must be >= 1 (got {args.gpus})", file=sys.stderr)
+        return 2
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        return launch_ranks(args, kw)   # N fresh rank processes; this one never touches the GPU
+    world = int(env_world or "1")
+    if world != args.gpus:   # an external launcher's world must be the one the line will report
+        print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # the CPU baseline is rank 0's report, measured before the GPU is initialised (forked workers, host
+    # cores otherwise idle); under bench.py's own launcher the parent measured it before starting the ranks
+    cpu, launcher = None, os.environ.get("SNG_BENCH_LAUNCHER", "external" if env_world else "none (N = 1)")
+    if rank == 0 and not args.no_cpu_baseline:
+        if os.environ.get("SNG_BENCH_CPU_BASELINE"):
+            with open(os.environ["SNG_BENCH_CPU_BASELINE"]) as fp:
+                cpu = json.load(fp)
+        else:
+            cpu = cpu_baseline(kw, args.cpu_budget)
     dist = None
     # one GPU per rank; ranks beyond the visible GPUs share them (gloo only: RCCL needs one rank per GPU).
     # torch.cuda.device_count() does not initialise the GPU on this image.
     ndev = max(1, torch.cuda.device_count())
+    if world > 1 and args.dist_backend == "nccl" and ndev < world:
+        print(f"bench.py: {world} RCCL ranks need {world} visible GPUs; {ndev} visible", file=sys.stderr)
+        return 2
     gpu = local % ndev
+    dist_info = {"backend": None, "world_size": 1, "launcher": launcher}
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(gpu)
@@ -249,6 +307,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group("gloo")
+        dist_info = {"backend": dist.get_backend(), "world_size": dist.get_world_size(), "launcher": launcher}
+        assert dist_info["world_size"] == args.gpus
     device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
     coll_dev = device if args.dist_backend == "nccl" else None   # where the collectives' tensors live
@@ -391,14 +451,15 @@ def main():
                                if args.dist_backend == "nccl" else
                                ", gloo all-gather of every day's returns staged through host memory, one per replay")
                               if world > 1 else "")},
-               "roofline": roof, "cpu_baseline": cpu}
+               "dist": dist_info, "roofline": roof, "cpu_baseline": cpu}
         print(json.dumps(out))
     for gr in graphs:
         gr.close()
     venv.close()
     if dist is not None:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define SNG_ABI_VERSION 9
+#define SNG_ABI_VERSION 10
 
 typedef enum SngStatus {
     SNG_OK = 0,
@@ -321,16 +321,6 @@ int sng_get_day_counter(SngEnv *env, uint64_t *out, void *stream);
  * them).  Allocates and frees its buffers; synchronises `stream`.  No reference counterpart. */
 int sng_bandwidth_probe(int device, int64_t read_bytes, int64_t write_bytes, int32_t reps, float *dispatch_us,
                         float *back_to_back_us, void *stream);
-
-/* The reference's rule-based controller (solvers/RBC/rbc.py:6-29) as one kernel over a batch of
- * observations of a PV station (the layout sng_step writes: [solar, price, solar x3, price x3, SoC x N,
- * departure x N, (BESS)]): per charger c, departure entry d_c == 0 -> 0, 0 < d_c < 0.16667 -> 1 (leaves
- * within 4 h), else (solar[t] + solar[t+1]) / 2; the BESS action (with_bess) is 0.  obs [num_envs][2N+8
- * (+1)] and actions [num_envs][N (+1)] f32, device memory; asynchronous on `stream`.  Replaces the
- * policy of the reference's RBC evaluation loop (solvers/RBC/rbc.py:4, evaluator.py:13-24), not a
- * reference ABI. */
-int sng_rule_based_actions(const float *obs, float *actions, int64_t num_envs, int32_t number_of_chargers,
-                           int32_t with_bess, void *stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Multi-GPU exchange: one process per GPU, each with its contiguous env shard

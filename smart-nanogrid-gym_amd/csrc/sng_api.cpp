@@ -42,7 +42,6 @@ hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, 
                              hipEvent_t b);
 hipError_t launch_ref_seed(const RefStreams &rs, uint64_t seed0, int64_t E, hipStream_t stream);
 hipError_t launch_mt_prepare(const RefStreams &rs, int64_t E, hipStream_t stream);
-hipError_t launch_rbc(const float *obs, float *act, int64_t E, int N, int bess, hipStream_t stream);
 hipError_t launch_ref_day(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
                           int i1, bool prepare, hipStream_t stream);
 int step_lanes_supported(int n, int lanes);
@@ -1933,17 +1932,6 @@ int sng_bandwidth_probe(int device, int64_t read_bytes, int64_t write_bytes, int
     if (e != hipSuccess) return fail(nullptr, SNG_ERR_HIP, std::string("sng_bandwidth_probe: ") + hipGetErrorString(e));
     if (dispatch_us) *dispatch_us = sum / reps * 1e3f;
     if (back_to_back_us) *back_to_back_us = ms / reps * 1e3f;
-    return SNG_OK;
-}
-
-int sng_rule_based_actions(const float *obs, float *actions, int64_t num_envs, int32_t number_of_chargers,
-                           int32_t with_bess, void *stream) {
-    if (!obs || !actions) return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "sng_rule_based_actions: null argument");
-    if (num_envs < 1 || number_of_chargers < 1 || number_of_chargers > kMaxChargers ||
-        num_envs * (int64_t)(number_of_chargers + 1) >= (int64_t)1 << 31)
-        return fail(nullptr, SNG_ERR_INVALID_ARGUMENT, "sng_rule_based_actions: bad sizes");
-    hipError_t e = launch_rbc(obs, actions, num_envs, number_of_chargers, with_bess ? 1 : 0, as_stream(stream));
-    if (e != hipSuccess) return fail(nullptr, SNG_ERR_HIP, std::string("sng_rule_based_actions: ") + hipGetErrorString(e));
     return SNG_OK;
 }
 

@@ -33,29 +33,7 @@ constexpr int kWave = 64;
 // Streaming (nontemporal) stores for the step's bulk outputs (SoC, observations): they leave
 // less dirty L2 for the end-of-kernel release (measured 8.92 -> 8.17 us per step at 65,536 x 10).
 #define SNG_ST(dst, v) __builtin_nontemporal_store((v), &(dst))
-#if defined(SNG_STAMPS) || defined(SNG_RD2_PROF)
-__device__ unsigned long long *g_stamps;   // diagnostic builds only: per-workgroup stamps / counters
-#endif
-#ifdef SNG_STAMPS
-// Diagnostic build only (make stamps): per-workgroup s_memrealtime stamps (100 MHz) at the
-// phase boundaries of the step kernel -> g_stamps[block*4 + k].  Never compiled into libsng.so.
-#define SNG_STAMP(k)                                                                                 \
-    do {                                                                                             \
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                  \
-        const unsigned long long ts_ = __builtin_amdgcn_s_memrealtime();                             \
-        if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 4 + (k)] = ts_;              \
-    } while (0)
-// The lean step kernel's stamps take no wait of their own: s_memrealtime when the wavefront reaches the
-// point, kept in registers and written by workgroup 0's first lane at the end -> g_stamps[block*8 + k].
-#define SNG_LSTAMP(k) stamp_[k] = __builtin_amdgcn_s_memrealtime()
-#else
-#define SNG_STAMP(k) \
-    do {             \
-    } while (0)
-#define SNG_LSTAMP(k) \
-    do {              \
-    } while (0)
-#endif
+#include "sng_diag_hooks.h"   // empty hooks in libsng.so (tools/diag builds fill them)
 
 // ---------------------------------------------------------------------------------
 // numpy pairwise_sum (loops_utils.h.src) for n <= 128, fed one element at a time in
@@ -468,15 +446,7 @@ template <bool FAST, bool RCP, bool NONNEG = false, bool PK = false>
 __device__ __forceinline__ ChargerResult charger_step(const Params &p, uint32_t w, double aux, double run, double req,
                                                       float a, int t, double rcap) {
     ChargerResult o;
-#ifdef SNG_MEMFLOOR
-    // diagnostic build only (make memfloor): same loads and stores, trivial arithmetic
-    o.q = 0.0;
-    o.pw = aux + (double)a;
-    o.soc = run + aux;
-    o.nx = 0u;
-    o.fl = 0u;
-    return o;
-#endif
+    SNG_DIAG_CHARGER(o, aux, run, a);
     const double margin = 0.05 * req;
     const double d = (req - run) * 10;
     const bool insufficient = (t > 0) && (w & W_PEN) && (run < req - margin);
@@ -730,10 +700,7 @@ struct StepConst {
 // Threads per workgroup of the lean step kernel: one wavefront (1,024 workgroups at E = 65,536).
 // A/B on one box (day of 65,536 x 10): 64 threads 6.33-6.38 us per step, 256 threads 6.47-6.55,
 // 128 threads 7.13-7.14 (tools/gpu_session.sh ablib).
-#ifndef SNG_LEAN_BLOCK
-#define SNG_LEAN_BLOCK 64
-#endif
-constexpr int kLeanBlock = SNG_LEAN_BLOCK;
+constexpr int kLeanBlock = 64;
 
 template <int NC>
 struct LeanLds {
@@ -752,10 +719,8 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
     using Lay = LeanLds<NC>;
     constexpr int KT = (Lay::A * kWave + 4 * kWave - 1) / (4 * kWave);
     extern __shared__ __attribute__((aligned(16))) float lds[];
-#ifdef SNG_STAMPS
-    unsigned long long stamp_[5];
-#endif
-    SNG_LSTAMP(0);
+    SNG_WSTAMP_DECL;
+    SNG_WSTAMP(0);
     const int Ad = p.act_dim, O = p.obs_dim;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave), lane = threadIdx.x % kWave;
     const int64_t e0 = (int64_t)blockIdx.x * kLeanBlock + (int64_t)wave * kWave;
@@ -816,7 +781,7 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
     }
     act_tile.commit(s_act, lane);
     wave_lds_fence();
-    SNG_LSTAMP(1);
+    SNG_WSTAMP(1);
 
     const float *a_row = s_act + lane * Ad;
     float *o_row = s_obs + lane * O;
@@ -862,14 +827,12 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
             n_neg += (pw < 0.0) ? 1 : 0;
             pmin = __builtin_fmin(pmin, ip ? pw : __builtin_inf());
             pos_other |= ip && !(av[c] > 0.0f);
-#ifndef SNG_LEAN_NOSB
             // chargers in order: charger c waits only for its own loads (vmcnt counts down charger
             // by charger) while the later chargers' loads are in flight
             __builtin_amdgcn_sched_barrier(0);
-#endif
         }
     }
-    SNG_LSTAMP(2);
+    SNG_WSTAMP(2);
     double p_ch = seq_pos, p_dis = seq_neg;
     if constexpr (NC >= 8) {
         const bool pos_slow = n_pos >= 8 && (pos_other || !(seq_pos <= pmin * 0x1.0p28));
@@ -898,13 +861,10 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
                         info.episode_return ? ret_l : 0.0, 0.0, reward, done);
     }
     wave_lds_fence();
-    SNG_LSTAMP(3);
+    SNG_WSTAMP(3);
     if (nw > 0) copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
-    SNG_LSTAMP(4);
-#ifdef SNG_STAMPS
-    if (threadIdx.x == 0 && g_stamps)
-        for (int i = 0; i < 5; ++i) g_stamps[(size_t)blockIdx.x * 8 + i] = stamp_[i];
-#endif
+    SNG_WSTAMP(4);
+    SNG_WSTAMP_FLUSH(stamp_, 5);
     // a device-RNG day's first step advances the day counter its reset read (generate_kernel); no-return
     // atomic, so nothing waits for it.  A replayed day (bump_day = 0) drew no counter value of its own.
     if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0)
@@ -931,13 +891,6 @@ __global__ __launch_bounds__(kLeanBlock) void step_lean_kernel(const float *__re
 //   - constants by value, one kernarg round trip before the loads, 1/cap by recip_cap, no LDS but the
 //     actions and observation tiles (40 KB per wavefront: four per CU).
 // ---------------------------------------------------------------------------------
-#ifndef SNG_WIDE_SB
-#define SNG_WIDE_SB 1
-#endif
-// chargers per scheduling group of the wide kernel's fast loop.  A/B (profiles/r03_ab_wide_sched_groups.txt):
-// config 5 22.6-22.7 us at 1 and 2, 22.8 at 5, 27.1 with no barrier in a lane's 25 chargers; the headline
-// within noise
-constexpr int kWideSB = SNG_WIDE_SB;
 
 template <int NC, int L>
 struct WideLds {
@@ -973,13 +926,6 @@ __device__ __forceinline__ double from_part(double x) {
 // fewer than 8 powers are numpy's in-order sum when one lane holds them all), the first lane adds the
 // other lanes' vehicle penalties after its own in charger order (Python's sum, penaliser.py:55), and the
 // rare exact-order paths run on the first lane over all chargers.
-// Waves per SIMD the register budget is sized for: L by default (every wave of the E = 65,536 grid resident
-// at once); SNG_WIDE_WPE (A/B builds) caps it.  Config 5 with four lanes per env and a 3-wave budget (166
-// VGPRs, no spills, 3 of the 4,096 waves per SIMD resident): 29.6-29.8 us against 23.4 us with two lanes
-// (profiles/r03_ab_config5_four_lanes.txt).
-#ifndef SNG_WIDE_WPE
-#define SNG_WIDE_WPE 4
-#endif
 // One group of WENVS envs of a wavefront: its loads (issue), then its step (run).  A wavefront steps G
 // groups: every group's loads are issued before the first group is stepped, so a group's arithmetic and
 // stores overlap the later groups' loads still in flight (G = 1: the whole wavefront is one group).
@@ -997,13 +943,10 @@ struct WideGroup {
     // the fast loop's charger step without the discharge branch (charger_step NONNEG) for the headline's
     // station (step 6.60-6.66 -> 6.53-6.56 us, profiles/r04_ab_nonneg.txt).  At N = 50 the compiler merges
     // several chargers' select masks ahead of the per-charger scheduling barriers and spills them (332
-    // v_readlane); with each charger's inputs pinned to its block (SNG_WIDE_PIN) it compiles to 5.5 % fewer
-    // VALU, and config 5 ran 22.62-22.69 against 22.47-22.54 us (profiles/r04_ab_config5_nonneg.txt): its
-    // step is bound by its bytes, so config 5 keeps the general form
-#ifndef SNG_NONNEG_MAX
-#define SNG_NONNEG_MAX 16
-#endif
-    static constexpr bool kNonneg = NC <= SNG_NONNEG_MAX;
+    // v_readlane); with each charger's inputs pinned to its block it compiles to 5.5 % fewer VALU, and
+    // config 5 ran 22.62-22.69 against 22.47-22.54 us (profiles/r04_ab_config5_nonneg.txt): its step is
+    // bound by its bytes, so config 5 keeps the general form
+    static constexpr bool kNonneg = NC <= 16;
     static constexpr int H = (NC - 2) / 2;
     static_assert(!kPairs || CPL == H + 1, "a lane's chargers: H from whole pairs and one from the last");
     // the lane's whole pairs are whole record quads too (H a multiple of 4: N = 10, 50), and the last pair is
@@ -1021,6 +964,7 @@ struct WideGroup {
     double fpv[4], fpr[4];
     uint32_t w[CPL];
     double aux[PK ? 1 : CPL], run_[CPL], req[REQ ? CPL : 1];
+    SNG_WSTAMP_DECL;   // diagnostic builds: 0 issue, 1 actions tile staged, 2 chargers, 3 env tail, 4 obs stores issued
 
     // the (per-lane, uniform) byte offsets of charger j of the lane in a [N][E] u32 plane: j * E in the uniform
     // part, except for the j some lane lacks (a ragged last lane) or the last pair's charger, where the
@@ -1037,6 +981,7 @@ struct WideGroup {
     // loads oldest-needed-first: the actions tile and the per-env values, then every charger's state
     __device__ __forceinline__ void issue(int64_t e0_, const float *act, int64_t E, int t, int vec_io, const Params &p,
                                           const DeviceState &s, const InfoPtrs &info, int lane) {
+        SNG_WSTAMP(0);
         const int le = lane / L, part = lane % L;
         e0 = e0_;
         nw = (E - e0) < WENVS ? (int)(E - e0) : WENVS;
@@ -1110,6 +1055,7 @@ struct WideGroup {
     __device__ __forceinline__ void run(const float *s_act, float *s_obs, float *obs, double *reward, uint8_t *done,
                                         int64_t E, int t, int vec_io, const StepConst &k, const Params &p,
                                         const DeviceState &s, const InfoPtrs &info, int lane) {
+        SNG_WSTAMP(1);
         const int Ad = p.act_dim, O = p.obs_dim;
         const int le = lane / L, part = lane % L;
         const bool leader = part == 0;
@@ -1158,9 +1104,6 @@ struct WideGroup {
                         qv[L > 1 ? j : 0] = 0.0;
                         continue;
                     }
-#ifdef SNG_WIDE_PIN
-                    asm volatile("" : "+v"(av[j]), "+v"(w[j]));   // A/B: pin the charger's inputs to its block
-#endif
                     const uint32_t capi = cap_field<PK>(w[j]);
                     const bool occ = (w[j] & W_OCC) != 0;
                     const ChargerResult r = charger_step<true, true, kNonneg, PK>(p, PK ? (w[j] & ~W_STATIC) : w[j],
@@ -1186,8 +1129,11 @@ struct WideGroup {
                     seq_pos += r.pw;   // >= 0 here (the float32 product of a >= 0, or 0.0): adding it is exact
                     n_pos += ip ? 1 : 0;
                     pmin = __builtin_fmin(pmin, ip ? r.pw : __builtin_inf());
-                    // chargers in order (groups of kWideSB): charger j waits only for its own loads
-                    if ((j + 1) % kWideSB == 0) __builtin_amdgcn_sched_barrier(0);
+                    // chargers in order: charger j waits only for its own loads.  A/B of scheduling groups
+                    // (profiles/r03_ab_wide_sched_groups.txt): config 5 22.6-22.7 us with one or two chargers
+                    // per group, 22.8 with five, 27.1 with no barrier in a lane's 25 chargers; the headline
+                    // within noise
+                    __builtin_amdgcn_sched_barrier(0);
                 }
             }
             // numpy sums fewer than 8 positive powers in order: one lane's running sum is that sum; two lanes'
@@ -1279,68 +1225,51 @@ struct WideGroup {
             p_ch = pos.result();
             p_dis = neg.result();
         }
+        SNG_WSTAMP(2);
         if (live && leader) {
             pen_v += (t == 0) ? pen0_l : 0.0;   // python index -1 slot; every per-charger term is 0 at t = 0
             env_tail<false, true>(p, s, info, e0, (uint32_t)le, el1, el8, t, ratio, p.bess ? bess_l : 0.0, bess_action,
                                   p_ch, p_dis, pen_v, 100.0 * (double)n_nonexist, fl, o_row, k.v, fpv, fpr,
                                   info.episode_return ? ret_l : 0.0, 0.0, reward, done, &bs);
         }
+        SNG_WSTAMP(3);
         wave_lds_fence();
         copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
+        SNG_WSTAMP(4);
     }
 };
-
-// Groups of envs per wavefront of the wide kernel (G, an A/B knob): G = 2 steps two groups of 32 envs per
-// wavefront (1,024 wavefronts at 65,536 envs, one per SIMD), each group's loads issued before the first group
-// is stepped.  Measured at N = 10 (A/B on one box, profiles/r04_ab_groups.txt): 8.62-8.64 us per step in the
-// graph against 6.68-6.71 us with one group (two wavefronts per SIMD), so one group is the default.
-#ifndef SNG_WIDE_G10
-#define SNG_WIDE_G10 1
-#endif
-__host__ __device__ constexpr int wide_groups(int NC) { return NC == 10 ? SNG_WIDE_G10 : 1; }
-__host__ __device__ constexpr int wide_waves(int L, int G) {
-    return (L / G) < 1 ? 1 : ((L / G) < SNG_WIDE_WPE ? L / G : SNG_WIDE_WPE);
-}
 
 // L lanes per env (1, 2 or 4): lane `part` of an env steps chargers [part * CPL, min(NC, (part + 1) * CPL)),
 // CPL = ceil(NC / L).  The env's lanes are adjacent (one DPP quad); the partial charging sums, counts and
 // minima combine exactly on the first lane (a sum the exactness test accepts is exact in any order, and
 // fewer than 8 powers are numpy's in-order sum when one lane holds them all), the first lane adds the
 // other lanes' vehicle penalties after its own in charger order (Python's sum, penaliser.py:55), and the
-// rare exact-order paths run on the first lane over all chargers.  G groups of 64 / L envs per wavefront.
-// Waves per SIMD the register budget is sized for: L / G (every wave of the E = 65,536 grid resident at
-// once); SNG_WIDE_WPE (A/B builds) caps it.  Config 5 with four lanes per env and a 3-wave budget (166
-// VGPRs, no spills, 3 of the 4,096 waves per SIMD resident): 29.6-29.8 us against 23.4 us with two lanes
-// (profiles/r03_ab_config5_four_lanes.txt).
-template <int NC, int L, int G, bool PK, bool REQ, bool NOISE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(wide_waves(L, G), wide_waves(L, G)))) void
+// rare exact-order paths run on the first lane over all chargers.  One group of 64 / L envs per wavefront;
+// the register budget is sized for L waves per SIMD (every wave of the E = 65,536 grid resident at once).
+// Measured and reverted (A/B on one box):
+//   - two groups of 32 envs per wavefront at N = 10 (1,024 wavefronts, each group's loads issued before the
+//     first group is stepped): 8.62-8.64 us per step in the graph against 6.68-6.71 us
+//     (profiles/r04_ab_groups.txt);
+//   - config 5 with four lanes per env and a 3-wave budget (166 VGPRs, no spills, 3 of the 4,096 waves per
+//     SIMD resident): 29.6-29.8 us against 23.4 us with two lanes (profiles/r03_ab_config5_four_lanes.txt).
+template <int NC, int L, bool PK, bool REQ, bool NOISE>
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(L, L))) void
 step_wide_kernel(const float *__restrict__ act, float *__restrict__ obs, double *__restrict__ reward,
                  uint8_t *__restrict__ done, int64_t E, int t, int vec_io, StepConst k, Params p, DeviceState s,
                  InfoPtrs info) {
     static_assert(L == 1 || L == 2 || L == 4, "one, two or four lanes per env");
-    static_assert(G == 1 || G == 2, "one or two groups per wavefront");
     using Grp = WideGroup<NC, L, PK, REQ, NOISE>;
     using Lay = WideLds<NC, L>;
     extern __shared__ __attribute__((aligned(16))) float lds[];
     const int lane = threadIdx.x;
-    float *s_obs = lds + G * Lay::ACT;   // [G] actions tiles, then the observation tile the groups share
-    // the groups as named objects, not an array (an array of them kept config 5's registers from being
-    // promoted: 188 VGPRs spilled at N = 50)
-    Grp g0, g1;
-    const int64_t e0 = (int64_t)blockIdx.x * G * Grp::WENVS;   // the grid covers E: the first group has an env
-    const bool second = G == 2 && e0 + Grp::WENVS < E;         // a second group past E (odd tail) is skipped
-    g0.issue(e0, act, E, t, vec_io, p, s, info, lane);
-    if constexpr (G == 2) g1.issue(second ? e0 + Grp::WENVS : e0, act, E, t, vec_io, p, s, info, lane);
-    g0.act_tile.commit(lds, lane);
-    if constexpr (G == 2) g1.act_tile.commit(lds + Lay::ACT, lane);
+    float *s_obs = lds + Lay::ACT;   // the actions tile, then the observation tile
+    Grp g;
+    const int64_t e0 = (int64_t)blockIdx.x * Grp::WENVS;   // the grid covers E: the wavefront has an env
+    g.issue(e0, act, E, t, vec_io, p, s, info, lane);
+    g.act_tile.commit(lds, lane);
     wave_lds_fence();
-    g0.run(lds, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
-    if constexpr (G == 2) {
-        if (second) {
-            wave_lds_fence();   // the first group's copy-out reads precede the second group's tile writes
-            g1.run(lds + Lay::ACT, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
-        }
-    }
+    g.run(lds, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
+    SNG_WSTAMP_FLUSH(g.stamp_, 5);
     if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_fetch_add(s.episode, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1455,11 +1384,7 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
     // Wide single-lane stations (several batches): batch b + 1's loads are issued before batch b is
     // computed, so they land while it computes instead of after it (the loop is not unrolled: the
     // prefetched registers are copied into the batch's at the top of the next iteration).
-    constexpr bool kPF = (L == 1) && !kRows && (NC > 0) && (CH < NC) && (NC % CH == 0)
-#ifdef SNG_WIDE_NOPF
-                         && false   // A/B build: batches loaded in turn
-#endif
-        ;
+    constexpr bool kPF = (L == 1) && !kRows && (NC > 0) && (CH < NC) && (NC % CH == 0);
     constexpr int PFN = kPF ? CH : 1;
     uint32_t wn[PFN];
     double auxn[PFN], runn[PFN], reqn[PFN];
@@ -1515,16 +1440,12 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
     act_tile.issue(act + e0 * A, nw * A, vec_io != 0, lane);
     // 4. per-charger state of the first batch
     load_state(cbeg);
-#ifdef SNG_STAMPS
-    if (threadIdx.x == 0 && g_stamps) g_stamps[(size_t)blockIdx.x * 4] = __builtin_amdgcn_s_memrealtime();
-#endif
 #pragma unroll
     for (int k = 0; k < RCP_PER_LANE; ++k) s_rcp[k * kWave + lane] = rcp_v[k];
     if (kRows && lane < CST_COUNT) s_cst[lane] = cst_v;
     const double *cst = kRows ? s_cst : cst_r;
     act_tile.commit(s_act, lane);
     wave_lds_fence();
-    SNG_STAMP(1);
 
     const float *a_row = s_act + le * A;
     float *o_row = s_obs + le * O;
@@ -1596,20 +1517,12 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
                 // 1/cap from the LDS table here, not ahead with the actions: it needs charger j's
                 // record, and reading every record's up front waited for all of them
                 // (wide stations: recip_cap instead of the LDS table, exact all the same -- div_by_cap)
-#ifdef SNG_X_WIDEDIV
-                rc[j] = kRows ? s_rcp[cap_field<PK>(w[j])] : 0.0;
-#else
                 rc[j] = kRows ? s_rcp[cap_field<PK>(w[j])] : recip_cap((double)cap_field<PK>(w[j]));
-#endif
                 // a packed day: the arrival SoC is the running SoC the step before stored (sng_layout.h)
                 const bool occ = (w[j] & W_OCC) != 0;
                 const uint32_t wj = PK ? (w[j] & ~W_STATIC) : w[j];
                 const double aux_j = PK ? 0.0 : aux[j];
-#ifdef SNG_X_WIDEDIV
-                const ChargerResult r = charger_step<FAST, kRows, false, PK>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
-#else
                 const ChargerResult r = charger_step<FAST, true, false, PK>(p, wj, aux_j, run[j], req[j], av[j], t, rc[j]);
-#endif
                 const SocOff so = soc_off(c, n, E, el8);
                 bst<kNT>(socv, so.v, (PK && !occ) ? (double)rec_soc(w[j]) : r.soc, so.s);
                 if (DIAG) {   // 'Charger power values' and the SOC[c, t] the day record holds
@@ -1689,13 +1602,11 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
                        o_row, cst, fpv, fpr, ret_prev, bess0, reward, done);
     }
     wave_lds_fence();
-    SNG_STAMP(2);
     copy_out<kWave>(obs + e0 * O, s_obs, nw * O, vec_io != 0, lane);
     // a device-RNG day's first step advances the day counter its reset read (generate_kernel);
     // nothing in this launch reads it (done last: at the top it perturbed the prologue's schedule).
     // A replayed day (bump_day = 0) drew no counter value of its own.
     if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0) *s.episode += 1;
-    SNG_STAMP(3);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1705,11 +1616,7 @@ __global__ __launch_bounds__(step_block(NC)) __attribute__((amdgpu_waves_per_eu(
 // ---------------------------------------------------------------------------------
 struct HashStream {
     uint32_t key, ctr;
-#ifdef SNG_GEN_CHEAP   // diagnostic build only: no hashing (timing floor of the generator's stores)
-    __device__ __forceinline__ uint32_t next() { return key ^ ((ctr++) * 0x9e3779b9u); }
-#else
     __device__ __forceinline__ uint32_t next() { return mix32(key + (ctr++) * 0x9e3779b9u); }
-#endif
 };
 
 __device__ __forceinline__ double u32_unit(uint32_t x) { return (double)x * 0x1.0p-32; }   // [0, 1)
@@ -2050,12 +1957,9 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 // at 65,536 x 10 (A/B, one box), the steps' code and state staying in L2.  Diagnostic builds
 // (tools/gpu_session.sh ablib) split the reset's time: without the t = 0 observation blocks 24.3-24.9 us
 // (they run beside the timeline blocks), without phase 1's draws 20.7, without the record stores 16-16.8.
-// SNG_GEN_POL: A/B builds only.  Write-through record stores (sc1 | nt, sc0 | sc1 | nt) left the day
-// and the reset unchanged (profiles/r03_ab_generator_store_policy.txt).
-#ifndef SNG_GEN_POL
-#define SNG_GEN_POL kNT
-#endif
-constexpr int kGenRecPol = SNG_GEN_POL;
+// Write-through record stores (sc1 | nt, sc0 | sc1 | nt) left the day and the reset unchanged (A/B,
+// profiles/r03_ab_generator_store_policy.txt).
+constexpr int kGenRecPol = kNT;
 // Timeline rows of the generator's grid (see generate_kernel): four rows of 64 envs per full charger quad; a
 // last partial quad of w = N mod 4 chargers has 256 / w envs per row (w = 1, 2: one or two rows), or 64 envs
 // with one lane in four idle (w = 3: four rows).
@@ -2088,9 +1992,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     const int u = (int)blockIdx.y - obs_rows;
     const uint64_t day = *s.episode;
     if (u < 0) {
-#ifndef SNG_GX_NOOBS   // diagnostic builds (tools/gpu_session.sh ablib) only: generator cost breakdown
         observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds, (int)blockIdx.y);
-#endif
         return;
     }
     const int full = 4 * (p.n / 4);                              // timeline rows of the full quads
@@ -2110,11 +2012,7 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     int tfree = 0, nv = 0;
     for (int v = 0; v < kDayVehicles - 1; ++v) {   // the last slot holds the sentinel
         if (tfree >= T) break;
-#ifdef SNG_GX_NOPH1
-        VehicleDraw d{tfree + 1, tfree + 7, 40u, (double)code_soc(4096u), 0u, 4096u};
-#else
         const VehicleDraw d = draw_vehicle(p, rng, tfree, i4, i10, i1);
-#endif
         if (d.ta >= T) break;
         s_veh[v * kGenBlock + tid] = ((uint32_t)d.ta << kVehArrShift) | (d.cap << P_CAP_SHIFT) | ((uint32_t)d.dep << P_DEP_SHIFT);
         s_car[v * kGenBlock + tid] = rec_carry(false, d.code);
@@ -2180,9 +2078,6 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
         const bool arr1 = (v1 >> kVehArrShift) == (uint32_t)(t + 1);   // step t + 1's vehicle arrives then
         const uint32_t carry = arr1 ? car1 : 0u;
         const uint32_t w_emp = (pen ? W_PEN : 0u) | carry;
-#ifdef SNG_GX_NOPH2
-        if ((occ ? w_occ : w_emp) == 0xdeadbeefu)
-#endif
         bst16<kGenRecPol>(rec + (size_t)(t + 1) * nE, el2, occ ? w_occ : w_emp, r2);
         // requested SoC timeline (sng_layout.h): Requested_SOC[c, t-1] at t >= 1 -- the step reads
         // it where W_PEN is set -- and Requested_SOC[c, T-1] in the t = 0 slot (written below)
@@ -2230,52 +2125,6 @@ hipError_t launch_probe_copy(const void *in, void *out, int64_t nr, int64_t nw, 
 }
 
 // ---------------------------------------------------------------------------------
-// The reference's rule-based controller (solvers/RBC/rbc.py:6-29): 256 (wide stations: 64) envs per block,
-// thread = env.
-// The block's observation rows (one contiguous run) come in through LDS with 16 B loads, the actions
-// leave through LDS with 16 B stores, as the step kernel stages its tiles.  Comparisons and the
-// average in float32, as numpy does on the float32 observation with a Python-float threshold (NEP 50).
-// ---------------------------------------------------------------------------------
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void rbc_kernel(const float *__restrict__ obs, float *__restrict__ act, int64_t E,
-                                                    int N, int A, int O, int vec_io) {
-    extern __shared__ __attribute__((aligned(16))) float lds[];
-    float *s_obs = lds, *s_act = lds + round4(BLOCK * O);
-    const int tid = threadIdx.x;
-    const int64_t e0 = (int64_t)blockIdx.x * BLOCK;
-    const int nblk = (int)((E - e0) < BLOCK ? (E - e0) : BLOCK);
-    copy_in<8, BLOCK>(s_obs, obs + e0 * O, nblk * O, vec_io != 0, tid);
-    __syncthreads();
-    if (tid < nblk) {
-        const float *o = s_obs + tid * O;
-        float *a = s_act + tid * A;
-        const float follow = (o[0] + o[2]) / 2.f;
-        for (int c = 0; c < N; ++c) {
-            const float d = o[8 + N + c];
-            a[c] = (d == 0.f) ? 0.f : (d > 0.f && d < 0.16667f) ? 1.f : follow;
-        }
-        if (A > N) a[N] = 0.f;   // the BESS action
-    }
-    __syncthreads();
-    copy_out<BLOCK>(act + e0 * A, s_act, nblk * A, vec_io != 0, tid);
-}
-
-hipError_t launch_rbc(const float *obs, float *act, int64_t E, int N, int bess, hipStream_t stream) {
-    const int A = N + (bess ? 1 : 0), O = 2 * N + 8 + (bess ? 1 : 0);
-    const int vec = ((reinterpret_cast<uintptr_t>(obs) | reinterpret_cast<uintptr_t>(act)) & 15) == 0;
-    const size_t lds256 = (size_t)(round4(256 * O) + round4(256 * A)) * 4;
-    if (lds256 <= 64 * 1024) {   // up to 20 chargers
-        hipLaunchKernelGGL(rbc_kernel<256>, dim3((unsigned)((E + 255) / 256)), dim3(256), lds256, stream, obs, act, E, N,
-                           A, O, vec);
-    } else {                     // wide stations: 64-env tiles (100 KB at the ABI's 128 chargers)
-        const size_t lds64 = (size_t)(round4(64 * O) + round4(64 * A)) * 4;
-        hipLaunchKernelGGL(rbc_kernel<64>, dim3((unsigned)((E + 63) / 64)), dim3(64), lds64, stream, obs, act, E, N, A,
-                           O, vec);
-    }
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------
 // launch wrappers (called from sng_api.cpp)
 // ---------------------------------------------------------------------------------
 // Optional start/stop events: hipExtLaunchKernel stamps them with the dispatch's own
@@ -2288,17 +2137,11 @@ struct LaunchEvents {
 // lanes per env: A/B at 65,536 x 10 x 24 (tools/ab_headline.sh, three runs each) 6.47-6.51 us per step
 // in the day graph vs 6.67-6.71 for the lean kernel, day 0.1749-0.1761 vs 0.1796-0.1803 ms; one lane per
 // env 6.75-6.79, four 8.15-8.23.  With V2X a discharging action is routine, and the lean kernel's LDS rows
-// keep numpy's order cheaper than the wide kernel's rolled re-read.  SNG_WIDE_N10=0 builds the lean path.
-#ifndef SNG_WIDE_N10
-#define SNG_WIDE_N10 1
-#endif
-#ifndef SNG_WIDE_L10
-#define SNG_WIDE_L10 2
-#endif
+// keep numpy's order cheaper than the wide kernel's rolled re-read.
 // The lean step kernel's configurations: a compile-time station of N <= 16, one lane per env, no
 // diagnostics, NumPy-2 promotion with a power-of-two dt, no stochastic profiles.
 static bool lean_step(const Params &p, bool diag) {
-    const bool nc = p.n == 1 || p.n == 2 || p.n == 4 || p.n == 8 || (p.n == 10 && (!SNG_WIDE_N10 || p.v2x)) ||
+    const bool nc = p.n == 1 || p.n == 2 || p.n == 4 || p.n == 8 || (p.n == 10 && p.v2x) ||
                     p.n == 16;
     return nc && !diag && !p.legacy && p.dt_pow2 && !p.noise && !(p.lanes == 2 || p.lanes == 4);
 }
@@ -2324,39 +2167,35 @@ static void launch_lean(const Params &p, const DeviceState &s, const InfoPtrs &i
 // The wide lean step kernel's configurations: N = 50 (BASELINE config 5's station), one lane per env, no
 // diagnostics, NumPy-2 promotion with a power-of-two dt; stochastic profiles allowed.
 static bool wide_step(const Params &p, bool diag) {
-    return (p.n == 50 || (SNG_WIDE_N10 && p.n == 10 && !p.noise && !p.v2x)) && !diag && !p.legacy && p.dt_pow2 &&
+    return (p.n == 50 || (p.n == 10 && !p.noise && !p.v2x)) && !diag && !p.legacy && p.dt_pow2 &&
            !(p.lanes == 2 || p.lanes == 4);
 }
 
 // Lanes per env of the wide lean step kernel: two (2,048 wavefronts at 65,536 envs, two per SIMD).
 // A/B at config 5 (tools/wide_ab.sh, two runs each): 1 lane 25.85-25.91 us per step in the day graph,
 // 2 lanes 22.54-22.62, 4 lanes 30.36-30.49 (128 VGPRs: 40 spilled to scratch).
-#ifndef SNG_WIDE_L
-#define SNG_WIDE_L 2
-#endif
-constexpr int kWideL = SNG_WIDE_L;
-__host__ __device__ constexpr int wide_lanes(int NC) { return NC == 10 ? SNG_WIDE_L10 : kWideL; }
+__host__ __device__ constexpr int wide_lanes(int) { return 2; }
 
 template <int NC>
 static void launch_wide(const Params &p, const DeviceState &s, const InfoPtrs &info, const Tables &tab,
                         const float *act, float *obs, double *reward, uint8_t *done, int64_t E, int t, int vec_io,
                         hipStream_t stream, const LaunchEvents *ev) {
-    constexpr int L = wide_lanes(NC), G = wide_groups(NC);
+    constexpr int L = wide_lanes(NC);
     StepConst k;
     for (int i = 0; i < CST_COUNT; ++i) k.v[i] = step_constant(&tab, t, i);
     const bool req = p.req_stream && !p.req_zero;
     const int v = (p.packed ? 4 : 0) | (req ? 2 : 0) | (p.noise ? 1 : 0);
     void (*kerns[8])(const float *, float *, double *, uint8_t *, int64_t, int, int, StepConst, Params, DeviceState,
                      InfoPtrs) = {
-        step_wide_kernel<NC, L, G, false, false, false>, step_wide_kernel<NC, L, G, false, false, true>,
-        step_wide_kernel<NC, L, G, false, true, false>,  step_wide_kernel<NC, L, G, false, true, true>,
-        step_wide_kernel<NC, L, G, true, false, false>,  step_wide_kernel<NC, L, G, true, false, true>,
-        step_wide_kernel<NC, L, G, true, true, false>,   step_wide_kernel<NC, L, G, true, true, true>};
+        step_wide_kernel<NC, L, false, false, false>, step_wide_kernel<NC, L, false, false, true>,
+        step_wide_kernel<NC, L, false, true, false>,  step_wide_kernel<NC, L, false, true, true>,
+        step_wide_kernel<NC, L, true, false, false>,  step_wide_kernel<NC, L, true, false, true>,
+        step_wide_kernel<NC, L, true, true, false>,   step_wide_kernel<NC, L, true, true, true>};
     auto kern = kerns[v];
     using Lay = WideLds<NC, L>;
-    constexpr int ENVS = Lay::WENVS * G;   // envs per wavefront
+    constexpr int ENVS = Lay::WENVS;   // envs per wavefront
     const dim3 grid((unsigned)((E + ENVS - 1) / ENVS)), block(kWave);
-    const uint32_t lds = (uint32_t)((size_t)(G * Lay::ACT + Lay::OBS) * 4);
+    const uint32_t lds = (uint32_t)((size_t)(Lay::ACT + Lay::OBS) * 4);
     if (ev)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,
                               vec_io, k, p, s, info);
@@ -2421,11 +2260,7 @@ static void launch_step_n(const Params &p, const DeviceState &s, const InfoPtrs 
     }
 }
 
-#if defined(SNG_STAMPS) || defined(SNG_RD2_PROF)
-extern "C" int sng_debug_set_stamps(unsigned long long *dev_ptr) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -1;
-}
-#endif
+SNG_DIAG_SET_STAMPS   // diagnostic builds: sng_debug_set_stamps
 
 int step_lanes_supported(int n, int lanes) {
     const bool multi = (n == 2 || n == 4 || n == 8 || n == 10 || n == 16 || n == 50);
@@ -2445,7 +2280,6 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
                        hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
     LaunchEvents evs{ev_start, ev_stop};
     const LaunchEvents *ev = (ev_start && ev_stop) ? &evs : nullptr;
-#if !defined(SNG_LEAN_OFF)
     if (lean_step(p, info_diag(info))) {
         launch_lean_n(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
         return hipGetLastError();
@@ -2457,7 +2291,6 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
             launch_wide<50>(p, s, info, tab, act, obs, reward, done, E, t, vec_io, stream, ev);
         return hipGetLastError();
     }
-#endif
     if (info_diag(info))
         launch_step_n<true>(p, s, info, act, obs, reward, done, E, t, vec_io, stream, ev);
     else
@@ -2468,15 +2301,13 @@ hipError_t launch_step(const Params &p, const DeviceState &s, const InfoPtrs &in
 // The name rocprofv3 reports for the step kernel launch_step would dispatch next (the template
 // arguments launch_step_n / launch_step_l / launch_step_t select).
 int step_kernel_name(const Params &p, const InfoPtrs &info, char *buf, int len) {
-#if !defined(SNG_LEAN_OFF)
     if (lean_step(p, info_diag(info)))
         return snprintf(buf, (size_t)len, "void sng::step_lean_kernel<%d, %s, %s>", p.n, p.packed ? "true" : "false",
                         (p.req_stream && !p.req_zero) ? "true" : "false");
     if (wide_step(p, info_diag(info)))
-        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %d, %d, %s, %s, %s>", p.n, wide_lanes(p.n),
-                        wide_groups(p.n), p.packed ? "true" : "false", (p.req_stream && !p.req_zero) ? "true" : "false",
+        return snprintf(buf, (size_t)len, "void sng::step_wide_kernel<%d, %d, %s, %s, %s>", p.n, wide_lanes(p.n),
+                        p.packed ? "true" : "false", (p.req_stream && !p.req_zero) ? "true" : "false",
                         p.noise ? "true" : "false");
-#endif
     int nc = 0, lanes = 1;
     switch (p.n) {
         case 2: case 4: case 8: case 10: case 16: case 50:
@@ -2521,23 +2352,13 @@ hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed,
                            float *obs, double *ep_return, int vec_io, hipStream_t stream, hipEvent_t ev_start,
                            hipEvent_t ev_stop) {
     const size_t veh = generate_lds_bytes(p.req_enabled != 0), tile = (size_t)round4(kObsEnvs * p.obs_dim) * 4;
-#ifndef SNG_GX_FUSE_MAX
-#define SNG_GX_FUSE_MAX (32 * 1024)
-#endif
-    const bool fused = tile <= SNG_GX_FUSE_MAX;   // up to 60 chargers (config 5's 50: 27.9 KB)
+    const bool fused = tile <= 32 * 1024;   // up to 60 chargers (config 5's 50: 27.9 KB)
     const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(gen_rows(p.n) + (fused ? kObsBlocks : 0))),
         block(kGenBlock);
-#ifdef SNG_GX_SMALL_LDS   // diagnostic builds only (with SNG_GX_NOOBS): the list's LDS alone
-    const size_t lds = veh;
-#else
     const size_t lds = (fused && tile > veh) ? tile : veh;
-#endif
     const bool req = p.req_enabled != 0;
-#ifndef SNG_GX_T96
-#define SNG_GX_T96 1
-#endif
     auto kern = p.T == 24 ? (req ? generate_kernel<24, true> : generate_kernel<24, false>)
-                : (SNG_GX_T96 && p.T == 96 && !req) ? generate_kernel<96, false>   // config 5's 15-minute day
+                : (p.T == 96 && !req) ? generate_kernel<96, false>   // config 5's 15-minute day
                 : (req ? generate_kernel<0, true> : generate_kernel<0, false>);
     if (fused && ev_start && ev_stop) {   // the one-launch reset, timed by its own dispatch timestamps
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev_start, ev_stop, 0u, p, s, seed, E, i4, i10, i1, obs,
@@ -2698,10 +2519,6 @@ struct MtRingT {
     int head, tail;   // stream words (from the current block's start) drawn / loaded into the ring
     int q0;           // the day's first word (mti at the start)
     int avail;        // stream blocks materialised: 0 .. avail - 1
-#ifdef SNG_RD2_PROF
-    unsigned long long prof_refill = 0;
-    unsigned prof_nrefill = 0, prof_dry = 0;
-#endif
     __device__ __forceinline__ const uint32_t *word_ptr(int q) const {
         const int k = q / kMtN;
         return blk + ((cur0 + k) & 1) * kMtN + (q - k * kMtN);
@@ -2715,17 +2532,6 @@ struct MtRingT {
     }
     // wave-uniform: lanes holding <= 64 words load the next 64 (tail stays a multiple of 4)
     __device__ __forceinline__ void refill() {
-#ifdef SNG_RD2_PROF
-        const unsigned long long t0_ = __builtin_amdgcn_s_memtime();
-        ++prof_nrefill;
-#endif
-        refill_();
-#ifdef SNG_RD2_PROF
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        prof_refill += __builtin_amdgcn_s_memtime() - t0_;
-#endif
-    }
-    __device__ __forceinline__ void refill_() {
         if (tail - head <= kRing / 2) {
             materialise(tail + kRing / 2 - 1);
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -2751,9 +2557,6 @@ struct MtRingT {
     }
     __device__ __forceinline__ uint32_t next() {
         if (head >= tail) {   // the ring ran dry inside one step: the word's aligned group straight in
-#ifdef SNG_RD2_PROF
-            ++prof_dry;
-#endif
             typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
             materialise(head);
             const int g = head & ~3;
@@ -2856,30 +2659,11 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
     const uint32_t el8 = (uint32_t)e * 8u;
     const size_t nE = (size_t)n * (size_t)E;
-#ifdef SNG_RD2_PROF
-    const unsigned long long k_start = __builtin_amdgcn_s_memrealtime();
-    unsigned long long acc1 = 0, acc2 = 0;
-    unsigned iters = 0;
-#endif
     for (int c = 0; c < n; ++c) {
         const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
-#ifdef SNG_RD2_PROF
-        const unsigned long long p1 = __builtin_amdgcn_s_memtime();
-#endif
         // phase 1: the charger's vehicles, one iteration per step that draws
         int t = 0, nv = 0;
-#ifdef SNG_RD2_NOPH1   // diagnostic builds only: fake vehicles, no stream draws
-        for (; t < T && nv < kRefVeh - 1; ++nv) {
-            s_veh[nv * ENVS + lane] = (uint32_t)t | (40u << W_CAP_SHIFT) | ((uint32_t)(t + i4 + (lane & 3)) << W_DEP_SHIFT);
-            s_soc[nv * ENVS + lane] = 0.5;
-            t = t + i4 + (lane & 3) + 2;
-        }
-        t = T;
-#endif
         while (t < T) {
-#ifdef SNG_RD2_PROF
-            ++iters;
-#endif
             rng.top_up();   // ballots over the lanes still drawing: each then holds > kRing / 4 words
             // the next kScan steps' arrival draws at once: the first that arrives, the free steps before
             // it consumed together
@@ -2974,11 +2758,6 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
         }
         s_veh[nv * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);   // sentinel: never arrives
         s_veh[(nv + 1 < kRefVeh ? nv + 1 : nv) * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);
-#ifdef SNG_RD2_PROF
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        const unsigned long long p2 = __builtin_amdgcn_s_memtime();
-        acc1 += p2 - p1;
-#endif
         // phase 2: the timeline (encode_day, sng_api.cpp): cur = the vehicle of step t until step t has
         // passed its departure step, nxt the one after it (read a step ahead); a stay of zero steps
         // (dep == arrival, possible when 4/dt < 1) still marks its arrival step STATIC, as the host
@@ -3004,14 +2783,10 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
             const uint32_t rem = occ ? dep - (uint32_t)tt : 0u;
             const bool pen = prev_rem - pen_lo <= pen_span;   // prev_rem = 0: empty at t-1
             const size_t plane = (size_t)tt * nE;
-#ifdef SNG_RD2_NOSTORE   // diagnostic builds only: the day's draws without its timeline stores
-            if (live && soc_cur == 12345.0) {
-#else
             // every lane stores: a lane that is not live mirrors a live one (the same env's stream, so
             // the same values to the same addresses), and straight-line stores let the compiler count
             // them in vmcnt instead of draining them before the next refill's words are read
             {
-#endif
                 // plain global stores (a uniform plane pointer + the env): one buffer descriptor per plane
                 // would not fit the SGPRs of the unrolled walk
                 const size_t row = plane + (size_t)c * (size_t)E;
@@ -3031,40 +2806,17 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
             req_nxt = adv ? req_nn : req_nxt;
         }
         if (REQ) bst(s.req, el8, prev_req, r8);   // slot 0: Requested_SOC[c, T-1]
-#ifdef SNG_RD2_PROF
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        acc2 += __builtin_amdgcn_s_memtime() - p2;
-#endif
     }
     if (live) rs.pos[e] = rng.position();
-#ifdef SNG_RD2_PROF
-    const unsigned long long k_end = __builtin_amdgcn_s_memrealtime();
-    if (threadIdx.x == 0 && g_stamps) {
-        unsigned long long *o = g_stamps + (size_t)blockIdx.x * 8;
-        o[0] = k_start;
-        o[1] = k_end;
-        o[2] = acc1;
-        o[3] = acc2;
-        o[4] = rng.prof_refill;
-        o[5] = rng.prof_nrefill;
-        o[6] = iters;
-    }
-    const unsigned dry = rng.prof_dry;
-    if (g_stamps && dry) atomicAdd(g_stamps + (size_t)blockIdx.x * 8 + 7, (unsigned long long)dry);
-#endif
 }
 
 __host__ __device__ constexpr size_t ref_day2_lds_bytes(bool req, int envs) {
     return (size_t)kRing * envs * 4 + (size_t)kRefVeh * envs * (4 + 8 + (req ? 8 : 0));
 }
 
-#ifndef SNG_REF2_ENVS
-#define SNG_REF2_ENVS 0   // 0: by population size (ref_day2_envs); A/B builds fix it
-#endif
 // Envs per wavefront of ref_day2_kernel: each wavefront's day is one serial chain (an env's stream is
 // consumed charger after charger), so small populations spread over more, thinner wavefronts.
 static int ref_day2_envs(int64_t E) {
-    if (SNG_REF2_ENVS) return SNG_REF2_ENVS;
     return E >= 65536 ? 64 : E >= 16384 ? 32 : E >= 4096 ? 16 : 8;
 }
 

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("SNG_LIBRARY", os.path.join(os.path.dirname(PKG_DIR), 
 DATA_DIR = os.path.join(PKG_DIR, "data")
 IRRADIANCE_FILE = os.path.join(DATA_DIR, "solar_irradiance_1min.f64")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 SNG_OK = 0
 RNG_REFERENCE = 0
 RNG_DEVICE = 1
@@ -143,8 +143,6 @@ EXPORTS = {
     "sng_get_day_counter": (ctypes.c_int, [_H, ctypes.POINTER(ctypes.c_uint64), _S]),
     "sng_bandwidth_probe": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                            ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float), _S]),
-    "sng_rule_based_actions": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
-                                              ctypes.c_int32, _S]),
     "sng_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p]),
     "sng_comm_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                                        ctypes.POINTER(ctypes.c_void_p)]),

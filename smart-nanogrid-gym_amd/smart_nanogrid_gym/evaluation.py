@@ -25,7 +25,6 @@ Differences from the reference scripts (deliberate, documented):
     (charging_station.py:119-136).  The unchanged single-env loop above reproduces that exactly:
     SmartNanogridEnv.reset(generate_new_initial_values=False) replays the env's last generated day.
 """
-import ctypes
 
 import numpy as np
 
@@ -103,8 +102,6 @@ class RuleBasedController:
         return np.asarray(action, dtype=np.float32)
 
     def __call__(self, obs):
-        if obs.is_cuda:   # one kernel (sng_rule_based_actions) instead of ~10 torch launches
-            return self._native(obs)
         N = self.NUMBER_OF_CHARGERS
         d = obs[:, self.k_dep:self.k_dep + N]
         follow = ((obs[:, 0:1] + obs[:, 2:3]) / 2).expand(-1, N)
@@ -113,20 +110,6 @@ class RuleBasedController:
         if self.bess:
             a = torch.cat([a, torch.zeros_like(a[:, :1])], dim=1)
         return a.to(torch.float32)
-
-    def _native(self, obs):
-        from ._native import check, lib
-        if obs.dtype != torch.float32 or not obs.is_contiguous():
-            obs = obs.to(torch.float32).contiguous()
-        E = obs.shape[0]
-        if obs.dim() != 2 or obs.shape[1] != self.k_dep + self.NUMBER_OF_CHARGERS + (1 if self.bess else 0):
-            raise ValueError(f"observations must have shape [B, {self.k_dep + self.NUMBER_OF_CHARGERS + self.bess}]")
-        act = torch.empty((E, self.act_dim), dtype=torch.float32, device=obs.device)
-        with torch.cuda.device(obs.device):
-            check(lib().sng_rule_based_actions(ctypes.c_void_p(obs.data_ptr()), ctypes.c_void_p(act.data_ptr()), E,
-                                               self.NUMBER_OF_CHARGERS, 1 if self.bess else 0,
-                                               ctypes.c_void_p(torch.cuda.current_stream(obs.device).cuda_stream)))
-        return act
 
     def predict(self, obs, state=None, episode_start=None, deterministic=True):
         obs = np.asarray(obs, dtype=np.float32)

@@ -1,5 +1,5 @@
-"""GPU: the step kernel the headline bench times -- `void sng::step_wide_kernel<10, 2, 1, true, false, false>`
-(N = 10, two lanes per env, one group of 32 envs per wavefront, no diagnostics, NumPy-2 / power-of-two dt fast path, packed device-RNG day
+"""GPU: the step kernel the headline bench times -- `void sng::step_wide_kernel<10, 2, true, false, false>`
+(N = 10, two lanes per env, 32 envs per wavefront, no diagnostics, NumPy-2 / power-of-two dt fast path, packed device-RNG day
 records) -- pinned directly to the CPU oracle.
 
 Device-RNG days (GPU generator, as in the bench) are exported in the reference's initial_values layout
@@ -22,12 +22,8 @@ pytestmark = pytest.mark.gpu
 
 from smart_nanogrid_gym import SmartNanogridVecEnv  # noqa: E402
 
-# the headline's step kernel: the wide kernel with two lanes per env; A/B builds (tools/ab_headline.sh) step
-# N = 10 with the lean kernel or another lane count
-BENCH_KERNELS = ("void sng::step_wide_kernel<10, 2, 2, true, false, false>",
-                 "void sng::step_wide_kernel<10, 2, 1, true, false, false>", "void sng::step_lean_kernel<10, true, false>",
-                 "void sng::step_wide_kernel<10, 1, 1, true, false, false>", "void sng::step_wide_kernel<10, 1, 2, true, false, false>",
-                 "void sng::step_wide_kernel<10, 4, 1, true, false, false>")
+# the headline's step kernel: the wide kernel with two lanes per env
+BENCH_KERNELS = ("void sng::step_wide_kernel<10, 2, true, false, false>",)
 KW = dict(number_of_chargers=10, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse",
           pv_system_available_in_model=True, battery_system_available_in_model=True)
 

@@ -130,3 +130,27 @@ def test_bench_world2_branch_on_one_gpu():
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["steps"] == 4 and out["value"] > 0
     assert out["config"]["envs_per_gpu"] == 4096 and "env-sharded x2" in out["config"]["parallelism"]
+    assert out["dist"] == {"backend": "gloo", "world_size": 2, "launcher": "external"}
+
+
+def test_bench_gpus2_launches_its_own_ranks():
+    """`bench.py --gpus 2` with no launcher measures the CPU baseline itself (a short
+    budget here), then starts two fresh rank processes (torch.distributed.run as a child) that share this
+    box's GPU over gloo.  Rank 0's line reports n_gpus 2, the initialised world size and the parent's
+    cpu_baseline."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
+           "--envs", "4096", "--dist-backend", "gloo", "--cpu-budget", "1", "--timing-days", "1"]
+    env = dict(os.environ, SNG_CPU_BASELINE_PROCS="2")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=root, env=env)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert r.returncode == 0 and len(lines) == 1, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and "env-sharded x2" in out["config"]["parallelism"]
+    assert out["dist"]["world_size"] == 2 and out["dist"]["backend"] == "gloo"
+    assert out["dist"]["launcher"].startswith("bench.py --gpus")
+    assert out["cpu_baseline"]["cores"] == 2 and out["cpu_baseline"]["value"] > 0

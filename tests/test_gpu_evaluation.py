@@ -91,35 +91,3 @@ def test_evaluate_models_same_days(rng):
             ref = _oracle_episode(ctl.select_action, seed + i)[0]
             assert final["rbc"][i] == sum(ref)   # both sum the day's rewards left to right in f64
     assert mean["full"] != mean["zeros"]
-
-
-@pytest.mark.parametrize("N,bess", [(4, True), (10, True), (10, False), (50, True), (128, False)])
-def test_native_rule_based_controller_equals_rbc(N, bess):
-    """sng_rule_based_actions (the controller's device path) against the controller's torch restatement of
-    solvers/RBC/rbc.py:6-29 on the CPU, bit for bit: departure entries exactly 0, at and around the
-    0.16667 threshold, and the environment's own observations; BESS entries 0."""
-    ctl = RuleBasedController(N, battery_system_available_in_model=bess)
-    O = 2 * N + 8 + (1 if bess else 0)
-    g = torch.Generator().manual_seed(N)
-    obs = torch.rand((3000, O), generator=g, dtype=torch.float32) * 1.8
-    dep = obs[:, 8 + N:8 + 2 * N]
-    th = torch.tensor(0.16667, dtype=torch.float32)
-    edge = torch.tensor([0.0, 0.0, th.item(), torch.nextafter(th, torch.tensor(0.0)).item(),
-                         torch.nextafter(th, torch.tensor(1.0)).item(), 1e-30, 1.0], dtype=torch.float32)
-    for k, val in enumerate(edge.tolist()):
-        dep[k * 100:(k + 1) * 100] = val
-    dep[1000:1500] = 0.0
-    want = ctl(obs)
-    got = ctl(obs.to("cuda:0")).cpu()
-    assert torch.equal(got, want)
-    if bess:
-        assert torch.all(got[:, -1] == 0)
-    # on the env's own observations
-    v = SmartNanogridVecEnv(512, seed=3, rng="device", number_of_chargers=N, battery_system_available_in_model=bess,
-                            time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
-    o = v.reset_tensors()
-    for t in range(6):
-        a = ctl(o)
-        assert torch.equal(a.cpu(), ctl(o.cpu()))
-        o, _, _ = v.step_tensors(a)
-    v.close()

@@ -1,4 +1,4 @@
-"""GPU: the step kernel BASELINE config 5's bench times -- `void sng::step_wide_kernel<50, L, 1, true, false, true>`
+"""GPU: the step kernel BASELINE config 5's bench times -- `void sng::step_wide_kernel<50, L, true, false, true>`
 (N = 50, 15-minute steps, extended day, stochastic PV / price profiles, packed device-RNG day records,
 no diagnostics) -- pinned to the CPU oracle.
 
@@ -26,7 +26,7 @@ from test_gpu_bench_kernel import actions, load_day  # noqa: E402
 CONFIG5 = dict(number_of_chargers=50, time_interval="15min", charging_mode="bounded",
                vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
                battery_system_available_in_model=True, extended_day=True, pv_noise=0.2, price_noise=0.1)
-WIDE_KERNEL = ("void sng::step_wide_kernel<50, ", ", 1, true, false, true>")   # <N, lanes, groups, PK, REQ, NOISE>
+WIDE_KERNEL = ("void sng::step_wide_kernel<50, ", ", true, false, true>")   # <N, lanes, PK, REQ, NOISE>
 
 
 @pytest.fixture(scope="module", autouse=True)

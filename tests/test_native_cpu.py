@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for s in syms:
         assert hasattr(L, s), s
     assert set(syms) == set(_native.EXPORTS), "ctypes binding out of sync with include/sng.h"
-    assert L.sng_abi_version() == 9
+    assert L.sng_abi_version() == 10
 
 
 def test_config_defaults_are_reference_constants():

@@ -7,7 +7,8 @@ the reference's evaluator (solvers/evaluator.py:13-24) runs:
 
     obs = reset();  repeat T times: a = policy(obs); obs, r, done = step(a)
 
-Policies (--policy): "rbc", the rule-based controller above (one HIP kernel per step), or "mlp", the
+Policies (--policy): "rbc", the rule-based controller above (its torch form: round 5 removed the
+controller's HIP kernel from libsng.so, SURVEY.md section 2 #20 puts it out of scope), or "mlp", the
 network SB3's PPO("MlpPolicy", ...) builds by default (solvers/RL/ppo_train.py:89-92; net_arch 64-64,
 tanh, deterministic predict = the action mean clipped to the Box), random-initialised in fp32 -- the
 loop a PPO rollout or evaluation runs on this env, with torch's GEMMs (hipBLASLt) in it.

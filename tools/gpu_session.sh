@@ -25,15 +25,14 @@ for s in $STEPS; do
     one)   run pytest_one 600 python -m pytest ${ONE_TESTS:-tests/test_gpu_recorder.py} -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    ablib) i=0; for l in ${AB_LIBS:-libsng_old libsng libsng_old libsng libsng_old libsng}; do i=$((i+1)); SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "ab${i}_$l" 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-}; done
+    ablib) i=0; for l in ${AB_LIBS:?AB_LIBS="libsng_<name> libsng ..." (tools/diag/Makefile ab)}; do i=$((i+1)); SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "ab${i}_$l" 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-}; done
            for f in $OUT/ab*_*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f) $(grep -o '"mean_launch_us": [0-9.]*' $f)"; done | tee -a $OUT/session.log ;;
     ab)    for a in ${AB_ARGS:-"--pipeline 0" "--pipeline 1"}; do run "bench_ab_${a// /_}" 300 python bench.py --no-cpu-baseline $a; done ;;
     sweep) for l in 1 2 4; do run bench_l$l 300 python bench.py --no-cpu-baseline --lanes $l; done ;;
     sq)    for l in ${SQ_LANES:-1 2}; do run sq_l$l 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/sq_l$l -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 --lanes $l; done ;;
     sqw)   run sq_wide 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU -d $OUT/sq_wide -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1
            run sq_wide5 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU -d $OUT/sq_wide5 -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 2 --warmup 1 --graph-days 1 --timing-days 1 ;;
-    lstamps) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so run lstamps 300 python tools/lean_stamps.py ;;
-    stamps) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so run stamps 300 python tools/stamps.py 1 2 4 ;;
+    stamps) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so run stamps 300 python tools/stamps.py ;;
     prof)  run prof_stats 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline ;;
     cfg5)  run bench_cfg5 600 python bench.py --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 --cpu-budget 12
            run prof_cfg5 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_cfg5 -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 ;;

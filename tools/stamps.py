@@ -1,11 +1,15 @@
-"""Per-wave phase timeline of the step kernel (diagnostic build libsng_stamps.so).
+"""Per-workgroup phase timeline of the step kernel (diagnostic build libsng_stamps.so, tools/diag).
 
-    make -C smart-nanogrid-gym_amd/csrc stamps
-    SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so python tools/stamps.py [lanes...]
+    make -C tools/diag stamps
+    SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so python tools/stamps.py [lanes]
 
-Stamps (s_memrealtime, 100 MHz) per workgroup: 0 = loads issued, 1 = actions staged and all
-loads landed (forced wait), 2 = env computed (obs in LDS), 3 = obs stored and drained.
-Prints, per lanes setting, the median/p90 of each phase and the spread of wave start times.
+lanes 0 (default) times the headline's kernel (step_wide_kernel, two lanes per env, 32 envs per
+one-wavefront workgroup); lanes 1 the lean kernel (64 envs per workgroup).  The stamps add no wait of
+their own (s_memrealtime, 100 MHz, when the workgroup's wavefront reaches the point): 0 = start,
+1 = actions tile staged (the tile and the per-env values landed), 2 = chargers done, 3 = env tail done
+(observation tile complete), 4 = observation stores issued.  The
+kernel's device time per step comes from the HIP-event probe of the same process, so the stretch after
+stamp 4 (store drain + end of kernel) is that time minus the last stamp.
 """
 import ctypes
 import os
@@ -21,39 +25,51 @@ from smart_nanogrid_gym import SmartNanogridVecEnv, _native  # noqa: E402
 
 
 def main():
-    lanes_list = [int(x) for x in sys.argv[1:]] or [1, 2]
     L = _native.lib()
     setter = getattr(L, "sng_debug_set_stamps")
     setter.argtypes = [ctypes.c_void_p]
-    E, N = 65536, 10
-    for lanes in lanes_list:
-        venv = SmartNanogridVecEnv(E, seed=3, rng="device", step_lanes_per_env=lanes, number_of_chargers=N,
-                                   time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
-        blocks = (E * lanes + 255) // 256   # 256-thread workgroups, 256 / lanes envs each
-        buf = torch.zeros(blocks * 4, dtype=torch.int64, device="cuda:0")
-        assert setter(ctypes.c_void_p(buf.data_ptr())) == 0
-        acts = torch.rand((24, E, N + 1), device="cuda:0")
-        acts[..., -1] = acts[..., -1] * 2 - 1
-        phases = []
-        for day in range(2):
-            venv.reset_tensors()
-            for t in range(24):
-                venv.step_tensors(acts[t])
-                torch.cuda.synchronize()
-                s = buf.view(blocks, 4).cpu().numpy().astype(np.float64) * 10.0   # ns
-                if day == 1:
-                    phases.append(s - s[:, :1].min())
-        ph = np.stack(phases)   # [24, blocks, 4]
-        start, land, comp, end = ph[..., 0], ph[..., 1], ph[..., 2], ph[..., 3]
-        q = lambda x: f"med {np.median(x) / 1e3:6.2f} p90 {np.percentile(x, 90) / 1e3:6.2f} us"
-        print(f"lanes={lanes} waves={blocks}")
-        print("  wave start (rel. first) ", q(start))
-        print("  loads landed            ", q(land - start))
-        print("  compute                 ", q(comp - land))
-        print("  obs store + drain       ", q(end - comp))
-        print("  last wave end (kernel)  ", q(end.max(axis=1)))
-        setter(ctypes.c_void_p(0))
-        venv.close()
+    E, N = int(os.environ.get("ENVS", 65536)), 10
+    lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    venv = SmartNanogridVecEnv(E, seed=3, rng="device", number_of_chargers=N, time_interval="1h",
+                               charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse",
+                               step_lanes_per_env=lanes)
+    print("kernel:", venv.step_kernel_name())
+    per_block = 32 if "step_wide_kernel" in venv.step_kernel_name() else 64
+    blocks = (E + per_block - 1) // per_block   # one wavefront per workgroup; 8 stamp slots per block
+    buf = torch.zeros(blocks * 8, dtype=torch.int64, device="cuda:0")
+    assert setter(ctypes.c_void_p(buf.data_ptr())) == 0
+    g = torch.Generator(device="cuda:0").manual_seed(1)
+    acts = torch.rand((24, E, N + 1), device="cuda:0", generator=g)
+    acts[..., -1] = acts[..., -1] * 2 - 1
+    acts = torch.where(torch.rand(acts.shape, device="cuda:0", generator=g) < 0.2, torch.zeros_like(acts), acts)
+    rows, ts = [], []
+    for day in range(3):
+        venv.reset_tensors()
+        for t in range(24):
+            venv.step_tensors(acts[t])
+            torch.cuda.synchronize()
+            if day > 0:
+                rows.append(buf.view(blocks, 8)[:, :5].cpu().numpy().astype(np.float64) * 10.0)   # ns
+                ts.append(t)
+    allph = np.stack(rows)                      # [steps, blocks, 5]
+    allph = allph - allph[..., :1].min(axis=1, keepdims=True)
+    ts = np.array(ts)
+    for label, sel in (("t = 0", ts == 0), ("t >= 1", ts > 0)):
+        print(f"--- {label}")
+        report(allph[sel])
+    ms = venv.time_step_kernels(acts, days=1)
+    print(f"HIP-event step time: t = 0 {ms[0] * 1e3:.3f} us, t >= 1 mean {np.mean(ms[1:]) * 1e3:.3f} us")
+    setter(ctypes.c_void_p(0))
+    venv.close()
+
+
+def report(ph):
+    q = lambda x: f"med {np.median(x) / 1e3:6.3f}  p10 {np.percentile(x, 10) / 1e3:6.3f}  p90 {np.percentile(x, 90) / 1e3:6.3f} us"
+    names = ["start (rel. first WG)", "tile + per-env landed", "chargers", "env tail", "obs stores issued"]
+    print(f"{'wave start':28s}", q(ph[..., 0]))
+    for k in range(1, 5):
+        print(f"{names[k]:28s}", q(ph[..., k] - ph[..., k - 1]))
+    print(f"{'last WG reaches stamp 4':28s}", q(ph[..., 4].max(axis=1)))
 
 
 if __name__ == "__main__":
