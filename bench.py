@@ -24,7 +24,8 @@ start-to-start time rocprofv3 reports for a graph's kernels.  The reset kernel's
 dispatch time of the step kernel (`eager_launch_us`, `frac_eager`) come from HIP start/stop events
 attached to every dispatch of eager days right after the timed region, on the stream the kernels run on.
 `frac_rocprof` is the same bytes over the average duration of that kernel in the committed
-rocprofv3 --kernel-trace --stats summary (profiles/), when one exists for this kernel.  Beside the
+rocprofv3 --kernel-trace --stats summary (profiles/) of this very build (`build_id`, sng_build_id(): the
+SHA-256 of the library's sources), null when none is committed for it.  Beside the
 SURVEY.md 8(d) fraction: `frac_layout` prices the bytes this layout actually moves (32N + 89 B per env-step;
 +4 B with --per-env-flags), `frac_pmc` the PMC-measured HBM bytes (`traffic`,
 from the committed passes, null if absent), and `copy_step_size` / `copy_1gib` are the measured ceiling
@@ -37,11 +38,9 @@ quota (sched_getaffinity shows the whole machine on a GPU box), measured before 
 the reference's own Python step() range from SURVEY.md section 6 beside it.
 """
 import argparse
-import glob
 import json
 import multiprocessing
 import os
-import re
 import sys
 import time
 
@@ -156,35 +155,39 @@ def cpu_baseline(kw, budget_s):
                                            "GPU box)"}}
 
 
-def rocprof_average_us(kernel, extended):
-    """Average duration (us) of `kernel` in the newest committed rocprofv3 --stats summary of this
-    configuration (profiles/rNN_kernel_stats[_config5].csv), with the file it came from."""
-    pat = "r*_kernel_stats_config5.csv" if extended else "r*_kernel_stats.csv"
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)),   # by round, then name (deterministic)
-                   key=lambda f: (int(re.search(r"r(\d+)_", os.path.basename(f)).group(1)), os.path.basename(f)))
-    for path in reversed(files):
-        with open(path) as fp:
+def rocprof_average_us(kernel, n_envs, chargers, build_id):
+    """Average duration (us) of `kernel` in a committed rocprofv3 --stats summary taken on this very build
+    (profiles/kernel_stats_index.json lists each summary with the build id of the library it measured,
+    tools/pmc_summary.py), with the file it came from; (None, None) when no summary of this build exists
+    (a stale summary of another build is never quoted)."""
+    try:
+        index = json.load(open(os.path.join(ROOT, "profiles", "kernel_stats_index.json")))
+    except (OSError, ValueError):
+        return None, None
+    for e in reversed(index):   # the newest summary of this build and workload
+        if e.get("build_id") != build_id or e.get("envs") != n_envs or e.get("chargers") != chargers:
+            continue
+        with open(os.path.join(ROOT, e["file"])) as fp:
             for line in fp:
                 if line.startswith(f'"{kernel}('):
                     cols = line.rsplit('",', 1)[1].split(",")
-                    return float(cols[2]) / 1e3, os.path.relpath(path, ROOT)
+                    return float(cols[2]) / 1e3, e["file"]
     return None, None
 
 
-def load_pmc_traffic(n_envs, chargers, kernel):
-    """Per-launch HBM bytes of the step kernel from the committed rocprofv3 PMC summary
-    (only when it was collected for this kernel instantiation and size)."""
+def load_pmc_traffic(n_envs, chargers, kernel, build_id):
+    """Per-launch HBM bytes of the step kernel from the committed rocprofv3 PMC summary, only when it was
+    collected on this build (its build id), for this kernel instantiation and size; else None."""
     path = os.path.join(ROOT, "profiles", "pmc_step_kernel.json")
-    if not os.path.exists(path):
-        return None
     try:
         d = json.load(open(path))
-        for e in (d if isinstance(d, list) else [d]):
-            if e.get("envs") == n_envs and e.get("chargers") == chargers and e.get("kernel") == kernel:
-                return e.get("bytes_per_launch")
-    except Exception:
-        return None
-    return None
+    except (OSError, ValueError):
+        return None, None
+    for e in reversed(d if isinstance(d, list) else [d]):
+        if (e.get("envs") == n_envs and e.get("chargers") == chargers and e.get("kernel") == kernel
+                and e.get("build_id") == build_id):
+            return e.get("bytes_per_launch"), e.get("source")
+    return None, None
 
 
 def copy_ceiling(device, read_bytes, write_bytes, reps=50):
@@ -408,8 +411,10 @@ def main():
         achieved = bpl / launch_s / 1e9
         rd, wr = step_kernel_bytes(N, noise, flags=args.per_env_flags)
         lpl = (rd + wr) * E
-        traffic = load_pmc_traffic(E, N, kernel)
-        rp_us, rp_file = rocprof_average_us(kernel, args.extended_day or noise)
+        from smart_nanogrid_gym._native import lib
+        build_id = lib().sng_build_id().decode()
+        traffic, traffic_src = load_pmc_traffic(E, N, kernel, build_id)
+        rp_us, rp_file = rocprof_average_us(kernel, E, N, build_id)
         # measured ceilings: the same copy kernel at this step's own read/write bytes (one dispatch) and at
         # 1 GiB (512 MiB each way)
         c_step = copy_ceiling(device, rd * E, wr * E)
@@ -424,7 +429,10 @@ def main():
                 "layout_bytes_per_launch": lpl,
                 "frac_layout": frac(lpl, launch_s),
                 "frac_pmc": None if traffic is None else frac(traffic, launch_s),
-                "traffic_source": "profiles/pmc_step_kernel.json (rocprofv3 FETCH_SIZE x2 gfx950 correction + WRITE_SIZE)",
+                "build_id": build_id,
+                "traffic_source": (f"profiles/pmc_step_kernel.json, entry of build {build_id}: {traffic_src}; "
+                                   "rocprofv3 FETCH_SIZE x2 gfx950 correction + WRITE_SIZE" if traffic is not None else
+                                   f"no PMC passes committed for build {build_id} (profiles/pmc_step_kernel.json)"),
                 "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src,
                 "eager_launch_us": round(eager_s * 1e6, 3), "reset_us": round(reset_us, 3),
                 "frac_eager": frac(bpl, eager_s), "frac_layout_eager": frac(lpl, eager_s),

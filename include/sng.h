@@ -172,6 +172,9 @@ typedef struct SngEnv SngEnv;
 typedef struct SngGraph SngGraph;
 
 int32_t sng_abi_version(void);
+/* The library's build id: the first 12 hex digits of the SHA-256 of its sources (csrc/Makefile).  The
+ * measurements committed under profiles/ name the build they were taken on by this id. */
+const char *sng_build_id(void);
 
 /* Fill `cfg` with the reference's defaults (N=8, '1h', b-pv, bounded, sparse). */
 void sng_config_defaults(SngConfig *cfg);

@@ -818,6 +818,10 @@ hipStream_t as_stream(void *s) { return (hipStream_t)s; }
 extern "C" {
 
 int32_t sng_abi_version(void) { return SNG_ABI_VERSION; }
+#ifndef SNG_BUILD_ID
+#define SNG_BUILD_ID "unversioned"   // built outside csrc/Makefile
+#endif
+const char *sng_build_id(void) { return SNG_BUILD_ID; }
 
 void sng_config_defaults(SngConfig *c) {
     std::memset(c, 0, sizeof *c);

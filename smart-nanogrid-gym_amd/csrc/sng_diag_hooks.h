@@ -13,12 +13,19 @@
 
 #if defined(SNG_DIAG_STAMPS)
 __device__ unsigned long long *g_stamps;
-#define SNG_WSTAMP_DECL unsigned long long stamp_[8]
+#define SNG_WSTAMP_DECL unsigned long long stamp_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
 #define SNG_WSTAMP(k) stamp_[k] = __builtin_amdgcn_s_memrealtime()
-#define SNG_WSTAMP_FLUSH(arr, n)                                                                 \
-    do {                                                                                         \
-        if (threadIdx.x == 0 && g_stamps)                                                        \
-            for (int i_ = 0; i_ < (n); ++i_) g_stamps[(size_t)blockIdx.x * 8 + i_] = (arr)[i_]; \
+// accumulating phase timers (ref_day2_kernel): t = SNG_WNOW(); ...; SNG_WACC(k, t) adds the elapsed ticks
+#define SNG_WNOW() __builtin_amdgcn_s_memrealtime()
+#define SNG_WACC(k, t0) stamp_[k] += __builtin_amdgcn_s_memrealtime() - (t0)
+// slots 0..n-1 the stamps, slot 6 the XCC id (HW_REG_XCC_ID), slot 7 HW_REG_HW_ID (CU, SE, SIMD, wave slot)
+#define SNG_WSTAMP_FLUSH(arr, n)                                                                       \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && g_stamps) {                                                            \
+            for (int i_ = 0; i_ < (n); ++i_) g_stamps[(size_t)blockIdx.x * 8 + i_] = (arr)[i_];       \
+            g_stamps[(size_t)blockIdx.x * 8 + 6] = __builtin_amdgcn_s_getreg((3 << 11) | 20);          \
+            g_stamps[(size_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);          \
+        }                                                                                              \
     } while (0)
 #define SNG_DIAG_SET_STAMPS                                                                         \
     extern "C" int sng_debug_set_stamps(unsigned long long *dev_ptr) {                              \
@@ -31,6 +38,10 @@ __device__ unsigned long long *g_stamps;
     } while (0)
 #define SNG_WSTAMP_FLUSH(arr, n) \
     do {                         \
+    } while (0)
+#define SNG_WNOW() 0ull
+#define SNG_WACC(k, t0) \
+    do {                \
     } while (0)
 #define SNG_DIAG_SET_STAMPS
 #endif

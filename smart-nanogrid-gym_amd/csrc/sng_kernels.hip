@@ -1252,8 +1252,10 @@ struct WideGroup {
 //     (profiles/r04_ab_groups.txt);
 //   - config 5 with four lanes per env and a 3-wave budget (166 VGPRs, no spills, 3 of the 4,096 waves per
 //     SIMD resident): 29.6-29.8 us against 23.4 us with two lanes (profiles/r03_ab_config5_four_lanes.txt).
+// Wavefronts per workgroup of the wide kernel, each with its own envs and LDS tiles (no workgroup barrier).
+__host__ __device__ constexpr int wide_wpb(int) { return 1; }
 template <int NC, int L, bool PK, bool REQ, bool NOISE>
-__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(L, L))) void
+__global__ __launch_bounds__(kWave * wide_wpb(NC)) __attribute__((amdgpu_waves_per_eu(L, L))) void
 step_wide_kernel(const float *__restrict__ act, float *__restrict__ obs, double *__restrict__ reward,
                  uint8_t *__restrict__ done, int64_t E, int t, int vec_io, StepConst k, Params p, DeviceState s,
                  InfoPtrs info) {
@@ -1261,14 +1263,17 @@ step_wide_kernel(const float *__restrict__ act, float *__restrict__ obs, double 
     using Grp = WideGroup<NC, L, PK, REQ, NOISE>;
     using Lay = WideLds<NC, L>;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    const int lane = threadIdx.x;
-    float *s_obs = lds + Lay::ACT;   // the actions tile, then the observation tile
+    constexpr int W = wide_wpb(NC);
+    const int wave = W > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : 0, lane = threadIdx.x % kWave;
+    float *s_act = lds + wave * (Lay::ACT + Lay::OBS);   // the wavefront's actions tile, then its observation tile
+    float *s_obs = s_act + Lay::ACT;
     Grp g;
-    const int64_t e0 = (int64_t)blockIdx.x * Grp::WENVS;   // the grid covers E: the wavefront has an env
+    const int64_t e0 = ((int64_t)blockIdx.x * W + wave) * Grp::WENVS;
+    if (W > 1 && e0 >= E) return;   // wave-uniform: a last workgroup's wavefronts past E (W = 1: the grid covers E)
     g.issue(e0, act, E, t, vec_io, p, s, info, lane);
-    g.act_tile.commit(lds, lane);
+    g.act_tile.commit(s_act, lane);
     wave_lds_fence();
-    g.run(lds, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
+    g.run(s_act, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
     SNG_WSTAMP_FLUSH(g.stamp_, 5);
     if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_fetch_add(s.episode, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2193,9 +2198,9 @@ static void launch_wide(const Params &p, const DeviceState &s, const InfoPtrs &i
         step_wide_kernel<NC, L, true, true, false>,   step_wide_kernel<NC, L, true, true, true>};
     auto kern = kerns[v];
     using Lay = WideLds<NC, L>;
-    constexpr int ENVS = Lay::WENVS;   // envs per wavefront
-    const dim3 grid((unsigned)((E + ENVS - 1) / ENVS)), block(kWave);
-    const uint32_t lds = (uint32_t)((size_t)(Lay::ACT + Lay::OBS) * 4);
+    constexpr int W = wide_wpb(NC), ENVS = Lay::WENVS * W;   // envs per workgroup
+    const dim3 grid((unsigned)((E + ENVS - 1) / ENVS)), block(kWave * W);
+    const uint32_t lds = (uint32_t)((size_t)W * (Lay::ACT + Lay::OBS) * 4);
     if (ev)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,
                               vec_io, k, p, s, info);
@@ -2659,8 +2664,12 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
     const uint32_t el8 = (uint32_t)e * 8u;
     const size_t nE = (size_t)n * (size_t)E;
+    // diagnostic builds: stamps 0 / 1 the kernel's start and end, 2 / 3 the ticks in phase 1 / phase 2
+    SNG_WSTAMP_DECL;
+    SNG_WSTAMP(0);
     for (int c = 0; c < n; ++c) {
         const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
+        [[maybe_unused]] const unsigned long long t1_ = SNG_WNOW();
         // phase 1: the charger's vehicles, one iteration per step that draws
         int t = 0, nv = 0;
         while (t < T) {
@@ -2758,6 +2767,8 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
         }
         s_veh[nv * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);   // sentinel: never arrives
         s_veh[(nv + 1 < kRefVeh ? nv + 1 : nv) * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);
+        SNG_WACC(2, t1_);
+        [[maybe_unused]] const unsigned long long t2_ = SNG_WNOW();
         // phase 2: the timeline (encode_day, sng_api.cpp): cur = the vehicle of step t until step t has
         // passed its departure step, nxt the one after it (read a step ahead); a stay of zero steps
         // (dep == arrival, possible when 4/dt < 1) still marks its arrival step STATIC, as the host
@@ -2806,8 +2817,11 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
             req_nxt = adv ? req_nn : req_nxt;
         }
         if (REQ) bst(s.req, el8, prev_req, r8);   // slot 0: Requested_SOC[c, T-1]
+        SNG_WACC(3, t2_);
     }
     if (live) rs.pos[e] = rng.position();
+    SNG_WSTAMP(1);
+    SNG_WSTAMP_FLUSH(stamp_, 4);
 }
 
 __host__ __device__ constexpr size_t ref_day2_lds_bytes(bool req, int envs) {

@@ -100,6 +100,7 @@ class SngScenario(ctypes.Structure):
 _H, _S = ctypes.c_void_p, ctypes.c_void_p   # handle, hipStream_t
 EXPORTS = {
     "sng_abi_version": (ctypes.c_int32, []),
+    "sng_build_id": (ctypes.c_char_p, []),
     "sng_config_defaults": (None, [ctypes.POINTER(SngConfig)]),
     "sng_create": (ctypes.c_int, [ctypes.POINTER(SngConfig), ctypes.c_int, ctypes.c_int64, ctypes.c_uint64,
                                   ctypes.POINTER(ctypes.c_void_p)]),

@@ -21,3 +21,26 @@ def test_layout_model_matches_pmc_traffic():
         assert abs(e["bytes_per_launch"] / model - 1) < 0.02, (e["kernel"], e["bytes_per_launch"], model)
         seen += 1
     assert seen >= 2
+
+
+def test_measurements_are_looked_up_by_build_id(tmp_path, monkeypatch):
+    """VERDICT r4 (weak 5): a committed PMC or rocprof summary is quoted only for the build it measured (its
+    sng_build_id()), never for another build that happens to keep the kernel's name."""
+    import bench
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    kernel = "void sng::step_wide_kernel<10, 2, true, false, false>"
+    (prof / "pmc_step_kernel.json").write_text(json.dumps([
+        dict(build_id="aaaaaaaaaaaa", kernel=kernel, envs=65536, chargers=10, bytes_per_launch=111, source="a"),
+        dict(build_id="bbbbbbbbbbbb", kernel=kernel, envs=65536, chargers=10, bytes_per_launch=222, source="b")]))
+    (prof / "r05_kernel_stats.csv").write_text(
+        '"Name","Calls","TotalDurationNs","AverageNs","Percentage","MinNs","MaxNs","StdDev"\n'
+        f'"{kernel}(float const*, float*)",100,640000,6400.0,90.0,6000,7000,10.0\n')
+    (prof / "kernel_stats_index.json").write_text(json.dumps([
+        dict(file="profiles/r05_kernel_stats.csv", build_id="aaaaaaaaaaaa", envs=65536, chargers=10)]))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.load_pmc_traffic(65536, 10, kernel, "bbbbbbbbbbbb") == (222, "b")
+    assert bench.load_pmc_traffic(65536, 10, kernel, "cccccccccccc") == (None, None)
+    assert bench.rocprof_average_us(kernel, 65536, 10, "aaaaaaaaaaaa") == (6.4, "profiles/r05_kernel_stats.csv")
+    assert bench.rocprof_average_us(kernel, 65536, 10, "bbbbbbbbbbbb") == (None, None)
+    assert bench.rocprof_average_us(kernel, 65536, 50, "aaaaaaaaaaaa") == (None, None)

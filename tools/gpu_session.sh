@@ -18,6 +18,9 @@ run() {  # run <name> <timeout> <cmd...>
   if fatal $rc; then echo "fatal exit $rc in $name; stopping" | tee -a $OUT/session.log; exit $rc; fi
   return 0
 }
+# the build id of the library the session measures (profiles/ are keyed by it: tools/pmc_summary.py, bench.py)
+python -c "import sys; sys.path.insert(0, 'smart-nanogrid-gym_amd'); from smart_nanogrid_gym import _native; print(_native.lib().sng_build_id().decode())" > $OUT/build_id.txt
+echo "=== build id $(cat $OUT/build_id.txt)" | tee -a $OUT/session.log
 STEPS="${STEPS:-tests smoke bench prof}"
 for s in $STEPS; do
   case $s in
@@ -33,6 +36,7 @@ for s in $STEPS; do
     sqw)   run sq_wide 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU -d $OUT/sq_wide -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1
            run sq_wide5 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_VALU -d $OUT/sq_wide5 -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 2 --warmup 1 --graph-days 1 --timing-days 1 ;;
     stamps) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so run stamps 300 python tools/stamps.py ;;
+    rdstamps) for l in ${RD_LIBS:-libsng_stamps}; do SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "rdstamps_$l" 300 python tools/rd_stamps.py; done ;;
     prof)  run prof_stats 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --no-cpu-baseline ;;
     cfg5)  run bench_cfg5 600 python bench.py --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 --cpu-budget 12
            run prof_cfg5 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_cfg5 -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 ;;
@@ -41,6 +45,8 @@ for s in $STEPS; do
     memfloor) SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_memfloor.so run memfloor 300 python bench.py --no-cpu-baseline
            SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_memfloor.so run memfloor_cfg5 300 python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 8 --warmup 2 ;;
     reset) run reset_bench 600 python tools/reset_bench.py ;;
+    resetab) i=0; for l in ${RESET_LIBS:?RESET_LIBS="libsng_<name> libsng ..."}; do i=$((i+1)); SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "reset${i}_$l" 300 python tools/reset_bench.py --envs 65536; done ;;
+    resetprof) run reset_prof 600 rocprofv3 --kernel-trace --stats -d $OUT/reset_prof -o run --output-format csv -- python tools/reset_bench.py --envs 65536 ;;
     layout) run stepmem2 300 tools/stepmem2 ;;
     sb3)   run sb3_path 600 python tools/sb3_path_bench.py
            run sb3_path_device 600 python tools/sb3_path_bench.py --rng device ;;

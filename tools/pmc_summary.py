@@ -6,7 +6,10 @@ Reads <out>/prof/run_kernel_stats.csv (--kernel-trace --stats) and the two PMC p
 <out>/pmc_fetch/run_counter_collection.csv (FETCH_SIZE) and <out>/pmc_write/... (WRITE_SIZE),
 writes profiles/<tag>_kernel_stats.csv, profiles/<tag>_pmc.csv and an entry of
 profiles/pmc_step_kernel.json; the same for config 5 from prof_cfg5/, pmc5_fetch/ and pmc5_write/
-(profiles/<tag>_kernel_stats_config5.csv, profiles/<tag>_pmc_config5.csv).
+(profiles/<tag>_kernel_stats_config5.csv, profiles/<tag>_pmc_config5.csv).  Every entry carries the build id of
+the library measured (<out>/build_id.txt, written by tools/gpu_session.sh; sng_build_id()), and the rocprof
+summaries are listed with theirs in profiles/kernel_stats_index.json: bench.py quotes only measurements of the
+build it runs.
 
 HBM bytes per launch (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and WRITE_SIZE are in KiB;
 on gfx950 FETCH_SIZE counts half the bytes of a coalesced streaming read, so
@@ -36,7 +39,13 @@ def main():
     out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "gpurun_out")
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
+    build_id = open(os.path.join(out, "build_id.txt")).read().strip()
     meta_path = os.path.join(prof, "pmc_step_kernel.json")
+    idx_path = os.path.join(prof, "kernel_stats_index.json")
+    try:
+        index = json.load(open(idx_path))
+    except (OSError, ValueError):
+        index = []
     try:
         entries = json.load(open(meta_path))
         entries = entries if isinstance(entries, list) else [entries]
@@ -48,7 +57,10 @@ def main():
         fpath = os.path.join(out, (pre or "pmc_") + "fetch", "run_counter_collection.csv")
         wpath = os.path.join(out, (pre or "pmc_") + "write", "run_counter_collection.csv")
         if os.path.exists(stats):
-            shutil.copyfile(stats, os.path.join(prof, f"{tag}_kernel_stats{suf}.csv"))
+            name = f"profiles/{tag}_kernel_stats{suf}.csv"
+            shutil.copyfile(stats, os.path.join(ROOT, name))
+            index = [e for e in index if e["file"] != name] + [
+                dict(file=name, build_id=build_id, envs=envs, chargers=chargers)]
         if not (os.path.exists(fpath) and os.path.exists(wpath)):
             continue
         fetch, nf = per_kernel(fpath, "FETCH_SIZE")
@@ -66,13 +78,15 @@ def main():
             wr.writerows(rows)
         step = [r for r in rows if "step_" in r["kernel"]][0]
         meta = dict(source=f"profiles/{tag}_pmc{suf}.csv (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes)",
-                    kernel=step["kernel"], envs=envs, chargers=chargers, bytes_per_launch=step["hbm_bytes_per_launch"],
+                    build_id=build_id, kernel=step["kernel"], envs=envs, chargers=chargers, bytes_per_launch=step["hbm_bytes_per_launch"],
                     fetch_kib=step["fetch_kib"], write_kib=step["write_kib"],
                     correction="traffic = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE counts half of streamed reads)")
-        entries = [e for e in entries if not (e.get("envs") == envs and e.get("chargers") == chargers)] + [meta]
+        entries = [e for e in entries if not (e.get("envs") == envs and e.get("chargers") == chargers
+                                              and e.get("build_id") == build_id)] + [meta]
         for r in rows:
             print(r)
     json.dump(entries, open(meta_path, "w"), indent=1)
+    json.dump(index, open(idx_path, "w"), indent=1)
 
 
 if __name__ == "__main__":

@@ -42,34 +42,63 @@ def main():
     acts = torch.rand((24, E, N + 1), device="cuda:0", generator=g)
     acts[..., -1] = acts[..., -1] * 2 - 1
     acts = torch.where(torch.rand(acts.shape, device="cuda:0", generator=g) < 0.2, torch.zeros_like(acts), acts)
-    rows, ts = [], []
+    rows, ts, ids = [], [], []
     for day in range(3):
         venv.reset_tensors()
         for t in range(24):
             venv.step_tensors(acts[t])
             torch.cuda.synchronize()
             if day > 0:
-                rows.append(buf.view(blocks, 8)[:, :5].cpu().numpy().astype(np.float64) * 10.0)   # ns
+                b = buf.view(blocks, 8).cpu().numpy()
+                rows.append(b[:, :5].astype(np.float64) * 10.0)   # ns
+                ids.append(b[:, 6:8])
                 ts.append(t)
     allph = np.stack(rows)                      # [steps, blocks, 5]
     allph = allph - allph[..., :1].min(axis=1, keepdims=True)
     ts = np.array(ts)
-    for label, sel in (("t = 0", ts == 0), ("t >= 1", ts > 0)):
+    for label, sel in (("eager t = 0", ts == 0), ("eager t >= 1", ts > 0)):
         print(f"--- {label}")
-        report(allph[sel])
+        report(allph[sel], np.stack(ids)[sel])
     ms = venv.time_step_kernels(acts, days=1)
     print(f"HIP-event step time: t = 0 {ms[0] * 1e3:.3f} us, t >= 1 mean {np.mean(ms[1:]) * 1e3:.3f} us")
+    # in a day graph (as the bench runs it): the stamps of the day's last step, t = T - 1
+    from smart_nanogrid_gym import EpisodeGraph
+    gr = EpisodeGraph(venv, acts.contiguous(), with_reset=True, days=1)
+    rows, ids = [], []
+    for rep in range(6):
+        gr.launch()
+        torch.cuda.synchronize()
+        if rep > 0:
+            b = buf.view(blocks, 8).cpu().numpy()
+            rows.append(b[:, :5].astype(np.float64) * 10.0)
+            ids.append(b[:, 6:8])
+    gr.close()
+    allph = np.stack(rows)
+    allph = allph - allph[..., :1].min(axis=1, keepdims=True)
+    print("--- graph, t = 23")
+    report(allph, np.stack(ids))
     setter(ctypes.c_void_p(0))
     venv.close()
 
 
-def report(ph):
+def report(ph, ids):
     q = lambda x: f"med {np.median(x) / 1e3:6.3f}  p10 {np.percentile(x, 10) / 1e3:6.3f}  p90 {np.percentile(x, 90) / 1e3:6.3f} us"
     names = ["start (rel. first WG)", "tile + per-env landed", "chargers", "env tail", "obs stores issued"]
     print(f"{'wave start':28s}", q(ph[..., 0]))
     for k in range(1, 5):
         print(f"{names[k]:28s}", q(ph[..., k] - ph[..., k - 1]))
     print(f"{'last WG reaches stamp 4':28s}", q(ph[..., 4].max(axis=1)))
+    st = ph[..., 0]
+    print("wave start deciles (us):", " ".join(f"{np.percentile(st, p) / 1e3:.2f}" for p in range(0, 101, 10)))
+    xcc = ids[..., 0] & 0xf
+    print("per XCC: median start / median stamp 4 (us):",
+          " ".join(f"{x}:{np.median(st[xcc == x]) / 1e3:.2f}/{np.median(ph[..., 4][xcc == x]) / 1e3:.2f}"
+                   for x in range(8) if (xcc == x).any()))
+    # block index order vs start: dispatch order
+    nb = st.shape[-1]
+    for part in range(4):
+        sl = slice(part * nb // 4, (part + 1) * nb // 4)
+        print(f"  blocks {sl.start}-{sl.stop - 1}: median start {np.median(st[..., sl]) / 1e3:.2f} us")
 
 
 if __name__ == "__main__":
