@@ -1251,11 +1251,12 @@ struct WideGroup {
 //     first group is stepped): 8.62-8.64 us per step in the graph against 6.68-6.71 us
 //     (profiles/r04_ab_groups.txt);
 //   - config 5 with four lanes per env and a 3-wave budget (166 VGPRs, no spills, 3 of the 4,096 waves per
-//     SIMD resident): 29.6-29.8 us against 23.4 us with two lanes (profiles/r03_ab_config5_four_lanes.txt).
-// Wavefronts per workgroup of the wide kernel, each with its own envs and LDS tiles (no workgroup barrier).
-__host__ __device__ constexpr int wide_wpb(int) { return 1; }
+//     SIMD resident): 29.6-29.8 us against 23.4 us with two lanes (profiles/r03_ab_config5_four_lanes.txt);
+//   - round 5: two or four such wavefronts per workgroup (each with its own envs and LDS tiles, no barrier;
+//     512 / 1,024 workgroups instead of 2,048): 6.79-6.80 / 6.99-7.03 us per step in the graph against
+//     6.31-6.34 us with one (profiles/r05_ab_waves_per_workgroup.txt).
 template <int NC, int L, bool PK, bool REQ, bool NOISE>
-__global__ __launch_bounds__(kWave * wide_wpb(NC)) __attribute__((amdgpu_waves_per_eu(L, L))) void
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(L, L))) void
 step_wide_kernel(const float *__restrict__ act, float *__restrict__ obs, double *__restrict__ reward,
                  uint8_t *__restrict__ done, int64_t E, int t, int vec_io, StepConst k, Params p, DeviceState s,
                  InfoPtrs info) {
@@ -1263,17 +1264,14 @@ step_wide_kernel(const float *__restrict__ act, float *__restrict__ obs, double 
     using Grp = WideGroup<NC, L, PK, REQ, NOISE>;
     using Lay = WideLds<NC, L>;
     extern __shared__ __attribute__((aligned(16))) float lds[];
-    constexpr int W = wide_wpb(NC);
-    const int wave = W > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x / kWave) : 0, lane = threadIdx.x % kWave;
-    float *s_act = lds + wave * (Lay::ACT + Lay::OBS);   // the wavefront's actions tile, then its observation tile
-    float *s_obs = s_act + Lay::ACT;
+    const int lane = threadIdx.x;
+    float *s_obs = lds + Lay::ACT;   // the actions tile, then the observation tile
     Grp g;
-    const int64_t e0 = ((int64_t)blockIdx.x * W + wave) * Grp::WENVS;
-    if (W > 1 && e0 >= E) return;   // wave-uniform: a last workgroup's wavefronts past E (W = 1: the grid covers E)
+    const int64_t e0 = (int64_t)blockIdx.x * Grp::WENVS;   // the grid covers E: the wavefront has an env
     g.issue(e0, act, E, t, vec_io, p, s, info, lane);
-    g.act_tile.commit(s_act, lane);
+    g.act_tile.commit(lds, lane);
     wave_lds_fence();
-    g.run(s_act, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
+    g.run(lds, s_obs, obs, reward, done, E, t, vec_io, k, p, s, info, lane);
     SNG_WSTAMP_FLUSH(g.stamp_, 5);
     if (PK && t == 0 && p.bump_day && blockIdx.x == 0 && threadIdx.x == 0)
         __hip_atomic_fetch_add(s.episode, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2198,9 +2196,9 @@ static void launch_wide(const Params &p, const DeviceState &s, const InfoPtrs &i
         step_wide_kernel<NC, L, true, true, false>,   step_wide_kernel<NC, L, true, true, true>};
     auto kern = kerns[v];
     using Lay = WideLds<NC, L>;
-    constexpr int W = wide_wpb(NC), ENVS = Lay::WENVS * W;   // envs per workgroup
-    const dim3 grid((unsigned)((E + ENVS - 1) / ENVS)), block(kWave * W);
-    const uint32_t lds = (uint32_t)((size_t)W * (Lay::ACT + Lay::OBS) * 4);
+    constexpr int ENVS = Lay::WENVS;   // envs per wavefront
+    const dim3 grid((unsigned)((E + ENVS - 1) / ENVS)), block(kWave);
+    const uint32_t lds = (uint32_t)((size_t)(Lay::ACT + Lay::OBS) * 4);
     if (ev)
         hipExtLaunchKernelGGL(kern, grid, block, lds, stream, ev->start, ev->stop, 0u, act, obs, reward, done, E, t,
                               vec_io, k, p, s, info);

@@ -48,6 +48,9 @@ for s in $STEPS; do
     resetab) i=0; for l in ${RESET_LIBS:?RESET_LIBS="libsng_<name> libsng ..."}; do i=$((i+1)); SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "reset${i}_$l" 300 python tools/reset_bench.py --envs 65536; done ;;
     resetprof) run reset_prof 600 rocprofv3 --kernel-trace --stats -d $OUT/reset_prof -o run --output-format csv -- python tools/reset_bench.py --envs 65536 ;;
     layout) run stepmem2 300 tools/stepmem2 ;;
+    sb3ab) for i in 1 2; do SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng.so run "sb3_old$i" 300 python tools/sb3_path_bench.py --pkg tools/diag/old_pkg
+                            run "sb3_new$i" 300 python tools/sb3_path_bench.py; done
+           run host_copy 120 python tools/host_copy_bench.py ;;
     sb3)   run sb3_path 600 python tools/sb3_path_bench.py
            run sb3_path_device 600 python tools/sb3_path_bench.py --rng device ;;
     pmc5)  run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc5_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 2 --warmup 1 --graph-days 1 --timing-days 1

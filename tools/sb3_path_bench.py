@@ -3,7 +3,7 @@ dones, infos) with numpy actions in and numpy results out, automatic reset at th
 default reference RNG (solvers/RL/ppo_train.py:89-102 hands the env to PPO, whose collect_rollouts calls
 env.step(clipped_actions) once per rollout step).
 
-    python tools/sb3_path_bench.py [--envs 65536] [--days 4] [--rng reference|device]
+    python tools/sb3_path_bench.py [--envs 65536] [--days 20] [--rng reference|device]
 
 Prints one JSON line: env-steps/s over whole days (the 24 steps of each day, its automatic reset included),
 and the split of one step into its phases, each the median over the timed steps:
@@ -12,8 +12,11 @@ and the split of one step into its phases, each the median over the timed steps:
   step        the step kernel (HIP events)
   d2h         the device -> pinned copy of the step's outputs (HIP events)
   sync        host time from the last enqueue until the stream is done
-  host_out    numpy copies of the results, infos list, flag checks
-  reset       the automatic reset of a done step (reference-RNG day + t = 0 observation to host), per day
+  host_out    the flag check and the host copies of the results
+  reset       the automatic reset of a done step, per day: reset_enqueue (the reset and its observation's
+              D2H copy queued), terminal_infos (the 65,536 terminal_observation infos, built while the
+              device resets), reset_wait (what is left of the device's work), reset_copy (the new day's
+              observations to a fresh array); reset_device = the reset + copy on the device (HIP events)
 Synthetic actions: uniform in the action Box, 20 % exact zeros, pre-generated host arrays (as a policy's
 numpy output arrives).  Steps are driven exactly as SB3 does, one env.step() per rollout step.
 """
@@ -34,10 +37,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--chargers", type=int, default=10)
-    ap.add_argument("--days", type=int, default=4, help="timed days")
+    ap.add_argument("--days", type=int, default=20, help="timed days")
     ap.add_argument("--warmup-days", type=int, default=1)
     ap.add_argument("--rng", default="reference", choices=["reference", "device"])
+    ap.add_argument("--pkg", default=None, help="A/B: the directory holding another smart_nanogrid_gym package")
     args = ap.parse_args()
+    if args.pkg:
+        sys.path.insert(0, os.path.abspath(args.pkg))
     from smart_nanogrid_gym import SmartNanogridVecEnv
     kw = dict(number_of_chargers=args.chargers, time_interval="1h", charging_mode="bounded",
               vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
@@ -69,7 +75,8 @@ def main():
            "value": E * n / elapsed, "unit": "env-steps/s", "envs": E, "chargers": args.chargers,
            "timesteps": T, "days": args.days, "rng": args.rng, "ms_per_step": elapsed / n * 1e3,
            "split_ms_median": split,
-           "note": "reset is per day (one automatic reset per 24 steps); every other phase per step"}
+           "note": "reset* are per day (one automatic reset per 24 steps); every other phase per step",
+           "reset_ms_per_day_mean": round(float(np.mean(ph["reset"])) * 1e3, 4) if ph.get("reset") else None}
     print(json.dumps(out))
     venv.close()
 
