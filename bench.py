@@ -261,6 +261,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: RCCL over xGMI (default), or gloo with the day returns staged through host "
                          "memory (several ranks on one GPU, tests)")
+    ap.add_argument("--v2x", action="store_true",
+                    help="a V2X station (vehicle_to_everything): Box actions in [-1, 1], so most envs hit the "
+                         "reference's V2X breakpoint every step (not the headline workload)")
     ap.add_argument("--per-env-flags", action="store_true",
                     help="time the step with the per-env per-step error-flag store of the diagnostics (the default "
                          "SngInfo watches the flag summary word instead)")
@@ -271,6 +274,8 @@ def main():
               vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
               battery_system_available_in_model=True)
     noise = args.pv_noise > 0 or args.price_noise > 0
+    if args.v2x:
+        kw.update(vehicle_to_everything=True)
     if args.extended_day or noise:
         kw.update(extended_day=args.extended_day, pv_noise=args.pv_noise, price_noise=args.price_noise)
     if args.gpus < 1:
@@ -348,18 +353,22 @@ def main():
     else:
         graphs = [EpisodeGraph(venv, acts, with_reset=True, days=D)]
     rep = [0]
+    host_launch_s = []   # host time of each replay's hipGraphLaunch (the host must keep ahead of the device)
 
     def day():   # one graph replay = D simulated days
         k = rep[0] % len(graphs)
         if xch is not None:
             xch.acquire(k)
+        h0 = time.perf_counter()
         graphs[k].launch()
+        host_launch_s.append(time.perf_counter() - h0)
         if xch is not None:
             xch.gather(k)
         rep[0] += 1
 
     for _ in range(-(-args.warmup // D)):   # at least W warmup days
         day()
+    host_launch_s.clear()
     if xch is not None:
         xch.finish()
     torch.cuda.synchronize()
@@ -434,6 +443,10 @@ def main():
                                    "rocprofv3 FETCH_SIZE x2 gfx950 correction + WRITE_SIZE" if traffic is not None else
                                    f"no PMC passes committed for build {build_id} (profiles/pmc_step_kernel.json)"),
                 "mean_launch_us": round(launch_s * 1e6, 3), "timing": timing_src,
+                # the host side of the timed replays: a wall time per day well above the device time per day
+                # means the host did not keep the GPU fed (one round-5 box: 0.25 against 0.17 ms)
+                "host_launch_ms_per_replay": round(float(np.median(host_launch_s)) * 1e3, 4),
+                "device_ms_per_day": round(day_gpu_us * 1e-3, 5),
                 "eager_launch_us": round(eager_s * 1e6, 3), "reset_us": round(reset_us, 3),
                 "frac_eager": frac(bpl, eager_s), "frac_layout_eager": frac(lpl, eager_s),
                 "copy_step_size": c_step, "copy_1gib": c_big,
@@ -442,10 +455,11 @@ def main():
                 "rocprof_avg_us": rp_us, "rocprof_file": rp_file,
                 "frac_rocprof": None if rp_us is None else frac(bpl, rp_us * 1e-6),
                 "frac_layout_rocprof": None if rp_us is None else frac(lpl, rp_us * 1e-6)}
-        headline = (N == 10 and T == 24 and not noise)
+        headline = (N == 10 and T == 24 and not noise and not args.v2x)
         metric = METRIC if headline else f"env-steps/sec (whole node) at N={E:,} envs × {N} chargers, {T}-step day"
-        desc = f"b-pv bounded sparse {args.time_interval}" + (
-            f", extended day, stochastic PV/price profiles (sigma {args.pv_noise}/{args.price_noise})" if not headline else "")
+        desc = ("v2x-" if args.v2x else "") + f"b-pv bounded sparse {args.time_interval}" + (
+            (", extended day" if args.extended_day else "") +
+            (f", stochastic PV/price profiles (sigma {args.pv_noise}/{args.price_noise})" if noise else ""))
         out = {"metric": metric, "value": value, "unit": "env-steps/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",

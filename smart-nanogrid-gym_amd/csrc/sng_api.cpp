@@ -622,7 +622,8 @@ int check_reference_seed(SngEnv *env) {
     const uint64_t last = env->seed + (uint64_t)env->p.env_offset + (uint64_t)(env->E - 1);
     if (env->seed >= (1ull << 32) || last >= (1ull << 32) || last < env->seed)
         return fail(env, SNG_ERR_INVALID_ARGUMENT,
-                    "reference RNG: seed + env offset + env index must be < 2^32 (np.random.seed's range)");
+                    "the reference's RNG streams (a reference-RNG day, or a PV ratio drawn for an injected or replayed "
+                    "day): seed + env offset + env index must be < 2^32 (np.random.seed's range)");
     return SNG_OK;
 }
 

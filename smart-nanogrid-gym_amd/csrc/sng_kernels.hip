@@ -548,6 +548,8 @@ __device__ __forceinline__ BessStep bess_step(const Params &p, const DeviceState
 // (central_management_system.py:99-185, penaliser.py:177-187, accountant.py:26-40) and the observation's
 // BESS entry.  Leader lane only.
 // ---------------------------------------------------------------------------------
+static_assert((SNG_FLAG_NEGATIVE_DEMAND | SNG_FLAG_CHARGING_MODE | SNG_FLAG_BESS_SOC_ABOVE_1 | SNG_FLAG_V2X_BREAKPOINT) == 0xfu,
+              "env_tail ORs the flag summary bit by bit: bits 0-3");
 template <bool DIAG, bool PRE = false>
 __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, const InfoPtrs &info, int64_t e0, uint32_t lo, uint32_t el1, uint32_t el8,
                                          int t, double ratio, double bess, float bess_action, double p_ch,
@@ -580,9 +582,16 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     // (the observation header was written before the chargers: step_kernel)
     if (p.bess && !PRE) o_row[p.obs_dim - 1] = (float)bess;
 
-    if (fl) {   // rare (sticky error bits); no-return atomics, nothing waits
-        atomicOr(s.flags + e0 + lo, fl);
-        if (info.flag_any) atomicOr(info.flag_any, fl);
+    if (fl) atomicOr(s.flags + e0 + lo, fl);   // sticky per-env error bits; no-return atomics, nothing waits
+    // the flag summary word: the wavefront's active lanes' bits ORed by one ballot per flag bit (four: sng.h),
+    // then one atomic per wavefront instead of one per flagged env to the same address (a V2X station flags
+    // most envs on most steps: ADVICE r4).  A wavefront without a flag pays one ballot.
+    if (info.flag_any && __builtin_amdgcn_ballot_w64(fl != 0u)) {
+        uint32_t any = 0u;
+#pragma unroll
+        for (uint32_t b = 1u; b <= SNG_FLAG_V2X_BREAKPOINT; b <<= 1)
+            any |= __builtin_amdgcn_ballot_w64((fl & b) != 0u) ? b : 0u;
+        if (__lane_id() == (unsigned)__builtin_ctzll(__builtin_amdgcn_read_exec())) atomicOr(info.flag_any, any);
     }
     if (info.flags) bst(info.flags, el1 * 4u, fl);
     if (info.episode_return) bst<kNT>(info.episode_return, el8, ret_prev + -total);

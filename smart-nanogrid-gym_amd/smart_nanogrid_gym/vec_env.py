@@ -290,8 +290,11 @@ class SmartNanogridVecEnv(_VecEnvBase):
         slots = 25, or T+1 with the build-defined extended day).  pv_ratio None: drawn per env from its
         Python stream."""
         self._check_mode()
+        seed = self._seed if self._seeds[0] is None else self._seeds[0]   # a pending seed() or the current one
+        if pv_ratio is None and seed is not None:   # (after load_state the blob's seed: the library checks it)
+            self._check_python_stream_seed(seed)
         self._apply_pending_seed()
-        arrs =[np.ascontiguousarray(a, np.float64) for a in (soc, occupancy, capacity, requested_soc)]
+        arrs = [np.ascontiguousarray(a, np.float64) for a in (soc, occupancy, capacity, requested_soc)]
         ai = np.ascontiguousarray(arrivals, np.int32)
         di = np.ascontiguousarray(departures, np.int32)
         sc = _native.SngScenario()
@@ -507,6 +510,15 @@ class SmartNanogridVecEnv(_VecEnvBase):
             raise ValueError("set_options: need one options dict per env")
         self._options = opts
 
+    def _check_python_stream_seed(self, seed):
+        """a day injected without pv_ratio draws each env's ratio from its Python stream,
+        random.seed(seed + env_offset + i), in every RNG mode; the streams are seeded as numpy's are, so the
+        last env's seed must stay below 2^32 here too (a device-RNG env accepts larger seeds otherwise)."""
+        if seed + self.env_offset + self.num_envs > 2 ** 32:
+            raise ValueError(f"seed {seed}: a day injected without pv_ratio draws env i's PV ratio from the Python "
+                             f"stream random.seed(seed + env_offset + i), which must stay below 2**32; pass pv_ratio "
+                             f"or use a seed in [0, {2 ** 32 - self.env_offset - self.num_envs}]")
+
     def _apply_pending_seed(self):
         if self._seeds[0] is None:
             return
@@ -697,6 +709,15 @@ class SmartNanogridVecEnv(_VecEnvBase):
         # before the restore would re-seed the restored streams and reset the day counter there
         self._seeds = [None] * self.num_envs
         self._options = [{} for _ in range(self.num_envs)]
+        # the blob's sticky per-env flags replace the handle's, so the summary word is rebuilt from
+        # them: a stale summary would report flags the restored day never raised, and restored flags that were
+        # never reported are raised (or reported as v2x_breakpoint infos) at the next step, as after any step
+        flags = np.zeros(self.num_envs, np.uint32)
+        with torch.cuda.device(self.device):
+            check(lib().sng_read_errors(self._h, flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 0,
+                                        _stream_handle(self.device)), self._h)
+            self.flag_summary_d.fill_(int(np.bitwise_or.reduce(flags)) if flags.size else 0)
+        self._flag_summary_h.zero_()
 
     # ------------------------------------------------------------------ the loaded day
     def get_scenarios(self, first=0, count=None, max_vehicles=8):

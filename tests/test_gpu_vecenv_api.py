@@ -361,3 +361,58 @@ def test_flag_summary_reports_errors_and_v2x_breakpoints():
     n.step_tensors(torch.zeros((E, 11), device=n.device))
     n.check_errors()   # cleared by the raise above: a clean step raises nothing
     n.close()
+
+
+def test_injected_day_checks_the_python_stream_seed_in_device_mode():
+    """a device-RNG env accepts a seed past numpy's range, but a day injected without pv_ratio draws
+    each env's ratio from random.seed(seed + env_offset + i): refused in Python with a message naming the
+    injected day, while an injected day with its ratios given works."""
+    E = 4
+    v = SmartNanogridVecEnv(E, seed=2 ** 32 - 2, rng="device", **KW)
+    v.reset_tensors()
+    iv, r = v.get_scenarios()
+    with pytest.raises(ValueError, match="pv_ratio"):
+        v.reset_from_initial_values(iv)
+    obs = v.reset_from_initial_values(iv, r)
+    assert np.isfinite(obs).all()
+    # the library's own check (the blob's seed is unknown to Python after load_state) names the same cause
+    blob = v.save_state()
+    v.load_state(blob)
+    with pytest.raises(NativeError, match="injected or replayed"):
+        v.reset_from_initial_values(iv)
+    v.close()
+
+
+def test_load_state_rebuilds_the_flag_summary():
+    """load_state replaces the sticky per-env flags, so the summary word follows them: a stale
+    summary does not survive the restore, and V2X flags the blob holds unreported (raised on the device path)
+    are reported at the next numpy step, for exactly the envs that raised them."""
+    E = 64
+    v2x = dict(KW, vehicle_to_everything=True)
+    a = SmartNanogridVecEnv(E, seed=2, rng="device", **v2x)
+    a.reset_tensors()
+    act = torch.zeros((E, 11), device="cuda:0")
+    act[: E // 2, :10] = -1.0   # the first half discharges: V2X demand < 0, flagged on the device
+    a.step_tensors(act)
+    pending = a.save_state()
+    want = np.zeros(E, np.uint32)
+    assert lib().sng_read_errors(a._h, want.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 0, None) == 0
+    want = (want & _native.FLAG_V2X_BREAKPOINT) != 0
+    assert want.any() and not want[E // 2:].any()
+    b = SmartNanogridVecEnv(E, seed=9, rng="device", **v2x)
+    b.reset_tensors()
+    clean = b.save_state()
+    b.flag_summary_d.fill_(_native.FLAG_V2X_BREAKPOINT)   # a stale summary from before the restore
+    b.load_state(clean)
+    assert int(b.flag_summary_d.cpu()[0]) == 0
+    _, _, _, infos = b.step(np.zeros((E, 11), np.float32))
+    assert not any("v2x_breakpoint" in d for d in infos)
+    b.load_state(pending)
+    assert int(b.flag_summary_d.cpu()[0]) & _native.FLAG_V2X_BREAKPOINT
+    _, _, _, infos = b.step(np.zeros((E, 11), np.float32))   # no new flag: idle chargers
+    got = np.array(["v2x_breakpoint" in d for d in infos])
+    np.testing.assert_array_equal(got, want)
+    _, _, _, infos = b.step(np.zeros((E, 11), np.float32))   # reported once: read and cleared
+    assert not any("v2x_breakpoint" in d for d in infos)
+    a.close()
+    b.close()

@@ -28,8 +28,9 @@ for s in $STEPS; do
     one)   run pytest_one 600 python -m pytest ${ONE_TESTS:-tests/test_gpu_recorder.py} -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
-    ablib) i=0; for l in ${AB_LIBS:?AB_LIBS="libsng_<name> libsng ..." (tools/diag/Makefile ab)}; do i=$((i+1)); SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "ab${i}_$l" 300 python bench.py --no-cpu-baseline ${BENCH_ARGS:-}; done
-           for f in $OUT/ab*_*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f) $(grep -o '"mean_launch_us": [0-9.]*' $f)"; done | tee -a $OUT/session.log ;;
+    ablib|ablib2) tag=${s/ablib/ab}; args=${BENCH_ARGS:-}; [ $s = ablib2 ] && args=${BENCH_ARGS2:-}
+           i=0; for l in ${AB_LIBS:?AB_LIBS="libsng_<name> libsng ..." (tools/diag/variant.sh)}; do i=$((i+1)); SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "${tag}-${i}_$l" 300 python bench.py --no-cpu-baseline $args; done
+           for f in $OUT/${tag}-*_*.log; do echo "$f $(grep -o '"ms_per_step": [0-9.]*' $f) $(grep -o '"mean_launch_us": [0-9.]*' $f)"; done | tee -a $OUT/session.log ;;
     ab)    for a in ${AB_ARGS:-"--pipeline 0" "--pipeline 1"}; do run "bench_ab_${a// /_}" 300 python bench.py --no-cpu-baseline $a; done ;;
     sweep) for l in 1 2 4; do run bench_l$l 300 python bench.py --no-cpu-baseline --lanes $l; done ;;
     sq)    for l in ${SQ_LANES:-1 2}; do run sq_l$l 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS -d $OUT/sq_l$l -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1 --lanes $l; done ;;
@@ -48,6 +49,7 @@ for s in $STEPS; do
     resetab) i=0; for l in ${RESET_LIBS:?RESET_LIBS="libsng_<name> libsng ..."}; do i=$((i+1)); SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "reset${i}_$l" 300 python tools/reset_bench.py --envs 65536; done ;;
     resetprof) run reset_prof 600 rocprofv3 --kernel-trace --stats -d $OUT/reset_prof -o run --output-format csv -- python tools/reset_bench.py --envs 65536 ;;
     layout) run stepmem2 300 tools/stepmem2 ;;
+    goverhead) run graph_overhead 300 tools/graph_overhead ;;
     sb3ab) for i in 1 2; do SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng.so run "sb3_old$i" 300 python tools/sb3_path_bench.py --pkg tools/diag/old_pkg
                             run "sb3_new$i" 300 python tools/sb3_path_bench.py; done
            run host_copy 120 python tools/host_copy_bench.py ;;
