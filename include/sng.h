@@ -63,6 +63,7 @@ typedef enum SngRngMode {
 } SngRngMode;
 
 /* Per-env flag bits reported by sng_read_errors / SngInfo.flags. */
+#define SNG_FLAG_SUMMARY_WORDS 1024   /* SngInfo.flag_summary's words */
 #define SNG_FLAG_NEGATIVE_DEMAND  0x1u  /* ValueError, central_management_system.py:158-159 */
 #define SNG_FLAG_CHARGING_MODE    0x2u  /* ValueError, charger.py:88/138, battery_energy_storage_system.py:74/106 */
 #define SNG_FLAG_BESS_SOC_ABOVE_1 0x4u  /* ValueError, penaliser.py:110-111 */
@@ -146,10 +147,13 @@ typedef struct SngInfo {
     /* per charger, [num_envs][N] (row-major, env-major); NULL = not written */
     double *charger_power;               /* 'Charger power values' (charging_station.py:282-299) */
     double *vehicle_soc;                 /* SOC[c, t] after the step (charger.py:37-56/:86/:136) */
-    /* device u32, NULL = not written: OR of the SNG_FLAG_* any env raised since the caller last zeroed it
-     * (one word, touched only when a flag is raised).  A caller that watches this word instead of `flags`
-     * spares the step its per-env flag store, and reads which envs raised what with
-     * sng_read_errors(clear = 1) only when the word is non-zero. */
+    /* device u32 [SNG_FLAG_SUMMARY_WORDS], NULL = not written: OR of the SNG_FLAG_* any env raised since the
+     * caller last zeroed it, spread over SNG_FLAG_SUMMARY_WORDS words (the envs of one wavefront share a
+     * word: word (first env of the wavefront / 32) mod SNG_FLAG_SUMMARY_WORDS), touched only when a flag is
+     * raised, one atomic per wavefront.  A caller that watches these words instead of `flags` spares the step
+     * its per-env flag store, and reads which envs raised what with sng_read_errors(clear = 1) only when a
+     * word is non-zero.  (One shared word made every flagged wavefront's atomic wait on the same address: a
+     * V2X station, which flags most envs every step, took ~10 us more per step at 65,536 envs.) */
     uint32_t *flag_summary;
 } SngInfo;
 

@@ -583,15 +583,20 @@ __device__ __forceinline__ void env_tail(const Params &p, const DeviceState &s, 
     if (p.bess && !PRE) o_row[p.obs_dim - 1] = (float)bess;
 
     if (fl) atomicOr(s.flags + e0 + lo, fl);   // sticky per-env error bits; no-return atomics, nothing waits
-    // the flag summary word: the wavefront's active lanes' bits ORed by one ballot per flag bit (four: sng.h),
-    // then one atomic per wavefront instead of one per flagged env to the same address (a V2X station flags
-    // most envs on most steps: ADVICE r4).  A wavefront without a flag pays one ballot.
+    // the flag summary (SngInfo.flag_summary): the wavefront's active lanes' bits ORed by one ballot per flag
+    // bit (four: sng.h), then one atomic per wavefront into the wavefront's own word.  A V2X station flags
+    // most envs on most steps: one atomic per flagged env into one shared word cost 18.9 us per
+    // step at N = 10, one per wavefront into that word 17.6 us -- the device-scope atomics on one address run
+    // one after another at the memory side, and the last wavefronts waited ~10 us for theirs
+    // (profiles/r05_stamps_v2x.txt) -- and one per wavefront into its own word 7.1 us.  A wavefront without a
+    // flag pays one ballot.
     if (info.flag_any && __builtin_amdgcn_ballot_w64(fl != 0u)) {
         uint32_t any = 0u;
 #pragma unroll
         for (uint32_t b = 1u; b <= SNG_FLAG_V2X_BREAKPOINT; b <<= 1)
             any |= __builtin_amdgcn_ballot_w64((fl & b) != 0u) ? b : 0u;
-        if (__lane_id() == (unsigned)__builtin_ctzll(__builtin_amdgcn_read_exec())) atomicOr(info.flag_any, any);
+        if (__lane_id() == (unsigned)__builtin_ctzll(__builtin_amdgcn_read_exec()))
+            atomicOr(info.flag_any + ((uint32_t)(e0 >> 5) & (SNG_FLAG_SUMMARY_WORDS - 1)), any);
     }
     if (info.flags) bst(info.flags, el1 * 4u, fl);
     if (info.episode_return) bst<kNT>(info.episode_return, el8, ret_prev + -total);

@@ -211,7 +211,7 @@ struct InfoPtrs {
     uint32_t *flags;
     double *episode_return;
     double *charger_power, *vehicle_soc;   // [E][N], DIAG only
-    uint32_t *flag_any;                    // SngInfo.flag_summary: OR of every raised flag (rare atomics)
+    uint32_t *flag_any;                    // SngInfo.flag_summary [SNG_FLAG_SUMMARY_WORDS]: OR of the raised flags
 };
 
 }  // namespace sng

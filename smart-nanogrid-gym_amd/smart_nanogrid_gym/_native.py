@@ -26,6 +26,7 @@ FLAG_NEGATIVE_DEMAND = 0x1
 FLAG_CHARGING_MODE = 0x2
 FLAG_BESS_SOC_ABOVE_1 = 0x4
 FLAG_V2X_BREAKPOINT = 0x8
+FLAG_SUMMARY_WORDS = 1024   # SngInfo.flag_summary words (sng.h SNG_FLAG_SUMMARY_WORDS)
 COMM_ID_BYTES = 128
 
 c_double_p = ctypes.POINTER(ctypes.c_double)

@@ -109,17 +109,18 @@ class SmartNanogridVecEnv(_VecEnvBase):
         self.actions_d = torch.zeros((E, self.act_dim), dtype=torch.float32, device=dev)
         # What the numpy (SB3) path brings back after every step, as one device block with one pinned host
         # mirror, so a step costs one device-to-host copy: reward f64 [E] | obs f32 [E][O] | done u8 [E] |
-        # the flag summary word (SngInfo.flag_summary), sections 256 B aligned.
+        # the flag summary words (SngInfo.flag_summary, 4 KiB), sections 256 B aligned.
         al = lambda x: (x + 255) // 256 * 256   # noqa: E731
         o_obs = al(E * 8)
         o_done = al(o_obs + E * O * 4)
         o_flag = al(o_done + E)
-        self._out_d = torch.zeros(o_flag + 256, dtype=torch.uint8, device=dev)
-        self._out_h = torch.zeros(o_flag + 256, dtype=torch.uint8, pin_memory=True)
+        W = _native.FLAG_SUMMARY_WORDS
+        self._out_d = torch.zeros(o_flag + 4 * W, dtype=torch.uint8, device=dev)
+        self._out_h = torch.zeros(o_flag + 4 * W, dtype=torch.uint8, pin_memory=True)
 
         def views(buf):
             return (buf[:E * 8].view(torch.float64), buf[o_obs:o_obs + E * O * 4].view(torch.float32).view(E, O),
-                    buf[o_done:o_done + E], buf[o_flag:o_flag + 4].view(torch.int32))
+                    buf[o_done:o_done + E], buf[o_flag:o_flag + 4 * W].view(torch.int32))
         self.reward_d, self.obs_d, self.done_d, self.flag_summary_d = views(self._out_d)
         self._rew_h, self._obs_h, self._done_h, self._flag_summary_h = views(self._out_h)
         self.flags_d = torch.zeros(E, dtype=torch.int32, device=dev)   # per-step flags, with info=True
@@ -450,7 +451,7 @@ class SmartNanogridVecEnv(_VecEnvBase):
         """After a step's outputs reached the host: None when no env raised a flag since the last check
         (the summary word, copied with the outputs, is 0), else the per-env SNG_FLAG_* raised since then
         (the sticky flags, read and cleared; the summary is zeroed)."""
-        if int(self._flag_summary_h.numpy()[0]) == 0:
+        if not self._flag_summary_h.numpy().any():
             return None
         return self._read_and_clear_flags()
 
@@ -716,7 +717,8 @@ class SmartNanogridVecEnv(_VecEnvBase):
         with torch.cuda.device(self.device):
             check(lib().sng_read_errors(self._h, flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 0,
                                         _stream_handle(self.device)), self._h)
-            self.flag_summary_d.fill_(int(np.bitwise_or.reduce(flags)) if flags.size else 0)
+            self.flag_summary_d.zero_()
+            self.flag_summary_d[0] = int(np.bitwise_or.reduce(flags)) if flags.size else 0
         self._flag_summary_h.zero_()
 
     # ------------------------------------------------------------------ the loaded day

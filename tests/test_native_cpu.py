@@ -159,3 +159,13 @@ def test_create_rejects_extended_day_without_flag():
     h = ctypes.c_void_p()
     rc = _native.lib().sng_create(ctypes.byref(cfg), 0, 4, 0, ctypes.byref(h))
     assert rc != 0 and b"extended_day" in _native.lib().sng_last_error(None)
+
+
+def test_python_constants_mirror_the_header():
+    """The flag bits and the flag-summary word count of include/sng.h, as the Python layer uses them."""
+    import re
+    text = open(os.path.join(ROOT, "include", "sng.h")).read()
+    defs = {k: int(v, 0) for k, v in re.findall(r"#define SNG_(FLAG_\w+)\s+(0x[0-9a-fA-F]+|\d+)u?", text)}
+    assert defs["FLAG_SUMMARY_WORDS"] == _native.FLAG_SUMMARY_WORDS
+    for k in ("FLAG_NEGATIVE_DEMAND", "FLAG_CHARGING_MODE", "FLAG_BESS_SOC_ABOVE_1", "FLAG_V2X_BREAKPOINT"):
+        assert defs[k] == getattr(_native, k), k

@@ -29,11 +29,15 @@ def main():
     setter = getattr(L, "sng_debug_set_stamps")
     setter.argtypes = [ctypes.c_void_p]
     E, N = int(os.environ.get("ENVS", 65536)), 10
-    lanes = int(sys.argv[1]) if len(sys.argv) > 1 else 0
+    v2x = "--v2x" in sys.argv   # a V2X station: the lean kernel, Box actions in [-1, 1]
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    lanes = int(args[0]) if args else 0
     venv = SmartNanogridVecEnv(E, seed=3, rng="device", number_of_chargers=N, time_interval="1h",
                                charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse",
-                               step_lanes_per_env=lanes)
+                               step_lanes_per_env=lanes, vehicle_to_everything=v2x)
     print("kernel:", venv.step_kernel_name())
+    venv.reset_tensors()
+    print("stepped by:", venv.step_kernel_name())
     per_block = 32 if "step_wide_kernel" in venv.step_kernel_name() else 64
     blocks = (E + per_block - 1) // per_block   # one wavefront per workgroup; 8 stamp slots per block
     buf = torch.zeros(blocks * 8, dtype=torch.int64, device="cuda:0")
@@ -41,6 +45,8 @@ def main():
     g = torch.Generator(device="cuda:0").manual_seed(1)
     acts = torch.rand((24, E, N + 1), device="cuda:0", generator=g)
     acts[..., -1] = acts[..., -1] * 2 - 1
+    if v2x:
+        acts = acts * 2 - 1
     acts = torch.where(torch.rand(acts.shape, device="cuda:0", generator=g) < 0.2, torch.zeros_like(acts), acts)
     rows, ts, ids = [], [], []
     for day in range(3):
