@@ -961,10 +961,6 @@ struct WideGroup {
     // config 5 ran 22.62-22.69 against 22.47-22.54 us (profiles/r04_ab_config5_nonneg.txt): its step is
     // bound by its bytes, so config 5 keeps the general form
     static constexpr bool kNonneg = NC <= 16;
-    // round 5: a wave with a discharging action (V2X) on a station stepped with the general charger_step (N = 50)
-    // runs the same loop and sums its kept powers in numpy's order, both lanes' powers gathered by DPP, instead
-    // of re-stepping every charger on the env's first lane from memory (V2X step at N = 50: 50.0 -> XX us)
-    static constexpr bool kPow = !kNonneg && L == 2 && NC % 4 == 2;
     static constexpr int H = (NC - 2) / 2;
     static_assert(!kPairs || CPL == H + 1, "a lane's chargers: H from whole pairs and one from the last");
     // the lane's whole pairs are whole record quads too (H a multiple of 4: N = 10, 50), and the last pair is
@@ -1108,17 +1104,12 @@ struct WideGroup {
 
         double pen_v = 0.0, p_ch = 0.0, p_dis = 0.0;
         uint32_t n_nonexist = 0, fl = 0;
-        const bool neg_wave = __builtin_amdgcn_ballot_w64(live && not_nonneg) != 0;
-        if (!neg_wave || kPow) {
-            // the loop: the lanes step their chargers.  A wave whose actions are all >= 0 has no negative power
-            // (p_dis stays 0.0) and its charging total is the running sum where exact (kNonneg stations step it
-            // with charger_step<..., NONNEG>); a wave with a discharging action (kPow stations only) keeps its
-            // powers and sums both signs in numpy's order after the loop
+        if (__builtin_amdgcn_ballot_w64(live && not_nonneg) == 0) {
+            // the fast loop: every action of the wave is >= 0, so no negative power (p_dis stays 0.0) and no
+            // charger discharges (charger_step<..., NONNEG>)
             double seq_pos = 0.0, pmin = __builtin_inf();
             int n_pos = 0;
-            double qv[L > 1 ? CPL : 1], sv[CPL], pwk[kPow ? CPL : 1];
-#pragma unroll
-            for (int j = 0; j < (kPow ? CPL : 1); ++j) pwk[j] = 0.0;
+            double qv[L > 1 ? CPL : 1], sv[CPL];
             if (live) {
 #pragma unroll
                 for (int j = 0; j < CPL; ++j) {
@@ -1148,9 +1139,8 @@ struct WideGroup {
                     // the lane's own penalties in charger order; kPairs: the last pair's come after the other
                     // lane's whole pairs (gather, below)
                     if (!kPairs || j < H) pen_v += r.q;
-                    if constexpr (kPow) pwk[j] = r.pw;
                     const bool ip = r.pw > 0.0;
-                    seq_pos += r.pw;   // a nonneg wave: >= 0 (the float32 product of a >= 0, or 0.0), adding it is exact
+                    seq_pos += r.pw;   // >= 0 here (the float32 product of a >= 0, or 0.0): adding it is exact
                     n_pos += ip ? 1 : 0;
                     pmin = __builtin_fmin(pmin, ip ? r.pw : __builtin_inf());
                     // chargers in order: charger j waits only for its own loads.  A/B of scheduling groups
@@ -1196,36 +1186,8 @@ struct WideGroup {
                 }
                 split = with_pos > 1;
             }
-            if constexpr (kPow) {
-                if (neg_wave) {
-                    // numpy's pairwise order for both signs (PairwiseSum) over the env's powers in charger order:
-                    // the first lane's whole pairs (chargers 0 .. H - 1), the second lane's (H .. 2H - 1), then
-                    // chargers N - 2 (first lane) and N - 1 (second lane); the second lane's powers come over by DPP
-                    PairwiseSum pos, neg;
-                    pos.init();
-                    neg.init();
-                    const bool sums = live && leader;
-                    auto push = [&](double v) {
-                        if (v > 0.0) pos.push(v);
-                        if (v < 0.0) neg.push(v);
-                    };
-#pragma unroll
-                    for (int j = 0; j < H; ++j)
-                        if (sums) push(pwk[j]);
-#pragma unroll
-                    for (int j = 0; j < H; ++j) {
-                        const double v = from_part<L, 1>(pwk[j]);
-                        if (sums) push(v);
-                    }
-                    if (sums) push(pwk[H]);
-                    const double v_last = from_part<L, 1>(pwk[H]);
-                    if (sums) push(v_last);
-                    p_ch = pos.result();
-                    p_dis = neg.result();
-                }
-            }
-            if (!neg_wave) p_ch = seq_pos;
-            const bool pos_slow = !neg_wave && live && leader && (n_pos >= 8 || split) && !(seq_pos <= pmin * 0x1.0p28);
+            p_ch = seq_pos;
+            const bool pos_slow = live && leader && (n_pos >= 8 || split) && !(seq_pos <= pmin * 0x1.0p28);
             if (__builtin_amdgcn_ballot_w64(pos_slow)) {   // wave-uniform: rare
                 if (pos_slow) {
                     // the compacted positive powers again, in charger order: an occupied charger charging with
@@ -1245,9 +1207,8 @@ struct WideGroup {
                 }
             }
         } else {
-            // a wave with a discharging action on a kNonneg station: numpy's pairwise order for both signs
-            // (PairwiseSum), one charger at a time on the env's first lane, its inputs re-read from memory and the
-            // actions tile (a V2X station of N = 10 steps through step_lean_kernel)
+            // a wave with a discharging action: numpy's pairwise order for both signs (PairwiseSum), one
+            // charger at a time on the env's first lane, its inputs re-read from memory and the actions tile
             PairwiseSum pos, neg;
             pos.init();
             neg.init();

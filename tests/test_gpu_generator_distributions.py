@@ -112,3 +112,22 @@ def test_device_generator_distributions(N, interval, E, days, ref_envs):
     _homogeneous(dep - arr, ref[:, 1] - ref[:, 0], "stay length")
     _homogeneous(arr, ref[:, 0], "arrival step")
     assert arr.min() >= 0 and arr.max() < T
+
+
+@pytest.mark.parametrize("N", [10, 50])
+def test_arrival_soc_codes(N):
+    """Device days carry the arrival SoC in their 2 B records as a 13-bit code (sng_layout.h code_soc): every
+    exported arrival SoC is one of the 8,192 float32 values 0.1f + 0.8f (k + 0.5) / 8192 and the draws cover that
+    grid evenly (the KS test above checks the law).  Round 5 measured 4 B records carrying any float32 value on
+    the headline station: 0.15-0.18 us more per step (profiles/r05_ab_records_4b.txt), so the grid stays."""
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+    v = SmartNanogridVecEnv(4096, seed=77, rng="device", **kw)
+    veh, _ = _vehicles_device(v, 2)
+    v.close()
+    soc = veh[:, 3]
+    assert soc.size > 20000 and np.all(soc == soc.astype(np.float32))
+    k = np.arange(8192, dtype=np.float32)
+    grid = np.float32(0.1) + np.float32(0.8) * ((k + np.float32(0.5)) * np.float32(1.0 / 8192.0))
+    assert np.isin(soc.astype(np.float32), grid).all()
+    counts = np.bincount(np.searchsorted(grid, soc.astype(np.float32)), minlength=8192)
+    assert stats.chisquare(counts).pvalue > P_MIN
