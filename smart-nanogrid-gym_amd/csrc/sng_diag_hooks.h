@@ -27,6 +27,11 @@ __device__ unsigned long long *g_stamps;
             g_stamps[(size_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);          \
         }                                                                                              \
     } while (0)
+// one slot written by thread tid of the workgroup (a second wavefront's own stamps)
+#define SNG_WSTAMP_PUT(slot, v, tid)                                                                   \
+    do {                                                                                               \
+        if ((int)threadIdx.x == (tid) && g_stamps) g_stamps[(size_t)blockIdx.x * 8 + (slot)] = (v);   \
+    } while (0)
 #define SNG_DIAG_SET_STAMPS                                                                         \
     extern "C" int sng_debug_set_stamps(unsigned long long *dev_ptr) {                              \
         return hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), &dev_ptr, sizeof(dev_ptr)) == hipSuccess ? 0 : -1; \
@@ -38,6 +43,9 @@ __device__ unsigned long long *g_stamps;
     } while (0)
 #define SNG_WSTAMP_FLUSH(arr, n) \
     do {                         \
+    } while (0)
+#define SNG_WSTAMP_PUT(slot, v, tid) \
+    do {                             \
     } while (0)
 #define SNG_WNOW() 0ull
 #define SNG_WACC(k, t0) \

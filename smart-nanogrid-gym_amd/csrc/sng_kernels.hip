@@ -2510,19 +2510,26 @@ __global__ __launch_bounds__(256) void mt_prepare_kernel(RefStreams rs, int64_t 
 // One env's numpy stream inside ref_day2_kernel: RandomState.random_sample / uniform / randint
 // (legacy, masked rejection) over the tempered words of the prepared blocks (sng_mt.h, host twin).
 //
-// The words reach the lane through a ring of 128 words in LDS, topped up for the whole wavefront at
+// The words reach the lane through a ring of 64 words in LDS, topped up for the whole wavefront at
 // once: the draws of a day are data-dependent (a free step draws two words, an arrival ~10), so the
 // 64 lanes of a wavefront desynchronise, and a global load per draw made every draw of every lane
-// wait out a memory round trip (0.53 ms per day at any population size).  Now a lane's draw is an
-// LDS read; when any lane's ring holds <= 32 words, every lane holding <= 64 loads the next 64 words
-// (16 aligned 16 B loads issued together, one wait), ~10-15 times a day.  A draw that finds the ring
-// empty (a rejection streak) loads its word directly.
+// wait out a memory round trip (0.53 ms per day at any population size).  A lane's draw is an LDS
+// read; when any lane's ring holds <= kTopUp words, every lane holding <= kRefill words commits the
+// next kRefill words into its ring.  Those words were loaded into registers one refill earlier (pf:
+// 8 aligned 16 B loads), so a refill waits for loads issued a refill ago, not for a fresh round trip:
+// the wavefront that draws issues no global stores (the timeline is the writer wavefront's, see
+// ref_day2_kernel), so nothing else is counted in vmcnt ahead of those loads.  A draw that finds the
+// ring empty (a rejection streak) refills its lane the same way.
 // Stream word q counts from the start of the day's current block: block k = q / 624 sits in slot
 // (cur0 + k) & 1, and a 4-word group never straddles two blocks (624 = 4 * 156).  Blocks 0 and 1 are
 // prepared (mt_prepare_kernel); a day that draws into block 2 or beyond twists it on its lane into the
-// slot of block k - 2, which the ring has consumed by then (it runs at most 128 words ahead).
+// slot of block k - 2, which the ring has consumed by then (it runs at most 96 words ahead: 64 in the
+// ring, 32 in registers).
 // LDS layout ring[slot][lane]: lanes reading any slots hit distinct banks.
-constexpr int kRing = 128;
+constexpr int kRing = 64;     // words per lane in LDS
+constexpr int kRefill = 32;   // words per refill (8 aligned 16 B groups)
+constexpr int kTopUp = 24;    // after a top_up every lane holds more than this: the peeks reach head + 21
+static_assert(kTopUp + kRefill <= kRing && kTopUp >= 22, "ring sizes (phase 1's peeks)");
 // RandomState.random_sample from two tempered words (numpy's rk_double: 53 bits, a >> 5 and b >> 6)
 __device__ __forceinline__ double rand53(uint32_t wa, uint32_t wb) {
     const int32_t a = (int32_t)(wa >> 5), b = (int32_t)(wb >> 6);
@@ -2530,16 +2537,14 @@ __device__ __forceinline__ double rand53(uint32_t wa, uint32_t wb) {
 }
 template <int ENVS>
 struct MtRingT {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     uint32_t *blk;
     uint32_t *ring;   // this lane's ring: ring[slot * ENVS], slot < kRing
     int cur0;
-    int head, tail;   // stream words (from the current block's start) drawn / loaded into the ring
+    int head, tail;   // stream words (from the current block's start) drawn / committed into the ring
     int q0;           // the day's first word (mti at the start)
     int avail;        // stream blocks materialised: 0 .. avail - 1
-    __device__ __forceinline__ const uint32_t *word_ptr(int q) const {
-        const int k = q / kMtN;
-        return blk + ((cur0 + k) & 1) * kMtN + (q - k * kMtN);
-    }
+    u32x4 pf[kRefill / 4];   // words [tail, tail + kRefill), loaded ahead of their refill
     __device__ __forceinline__ void materialise(int last) {   // blocks up to that of word `last`
         const int kmax = last / kMtN;
         while (avail <= kmax) {   // rare: a day of more than ~1,000 draws
@@ -2547,62 +2552,52 @@ struct MtRingT {
             ++avail;
         }
     }
-    // wave-uniform: lanes holding <= 64 words load the next 64 (tail stays a multiple of 4)
-    __device__ __forceinline__ void refill() {
-        if (tail - head <= kRing / 2) {
-            materialise(tail + kRing / 2 - 1);
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            u32x4 x[kRing / 8];
-            // the 64 words span at most two blocks: word q = tail + 4g is in block k0 up to offset 624
-            const int k0 = tail / kMtN, off0 = tail - k0 * kMtN;
-            const uint32_t *b0 = blk + ((cur0 + k0) & 1) * kMtN, *b1 = blk + ((cur0 + k0 + 1) & 1) * kMtN;
+    // pf <- words [tail, tail + kRefill): they span at most two blocks (word tail + 4g is in block k0 up to
+    // offset 624)
+    __device__ __forceinline__ void prefetch() {
+        materialise(tail + kRefill - 1);
+        const int k0 = tail / kMtN, off0 = tail - k0 * kMtN;
+        const uint32_t *b0 = blk + ((cur0 + k0) & 1) * kMtN, *b1 = blk + ((cur0 + k0 + 1) & 1) * kMtN;
 #pragma unroll
-            for (int g = 0; g < kRing / 8; ++g) {
-                const int off = off0 + 4 * g;
-                x[g] = *reinterpret_cast<const u32x4 *>(off < kMtN ? b0 + off : b1 + (off - kMtN));
-            }
-#pragma unroll
-            for (int g = 0; g < kRing / 8; ++g)
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    ring[((tail + 4 * g + i) & (kRing - 1)) * ENVS] = x[g][i];   // tempered in HBM
-            tail += kRing / 2;
+        for (int g = 0; g < kRefill / 4; ++g) {
+            const int off = off0 + 4 * g;
+            pf[g] = *reinterpret_cast<const u32x4 *>(off < kMtN ? b0 + off : b1 + (off - kMtN));
         }
     }
+    // the day's start: the ring is empty (tail = the first word's aligned group), its first words in flight
+    __device__ __forceinline__ void start(int mti) {
+        head = q0 = mti;
+        tail = mti & ~3;
+        avail = 2;
+        prefetch();
+    }
+    // this lane: the prefetched words into the ring (which then holds <= kRing), the next ones in flight
+    __device__ __forceinline__ void refill_lane() {
+#pragma unroll
+        for (int g = 0; g < kRefill / 4; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ring[((tail + 4 * g + i) & (kRing - 1)) * ENVS] = pf[g][i];   // tempered
+        tail += kRefill;
+        prefetch();
+    }
+    // wave-uniform test: lanes holding <= kRefill words refill, so every lane then holds > kTopUp
     __device__ __forceinline__ void top_up() {
-        if (__builtin_amdgcn_ballot_w64(tail - head <= kRing / 4)) refill();
+        if (__builtin_amdgcn_ballot_w64(tail - head <= kTopUp))
+            if (tail - head <= kRefill) refill_lane();
     }
     __device__ __forceinline__ uint32_t next() {
-        if (head >= tail) {   // the ring ran dry inside one step: the word's aligned group straight in
-            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-            materialise(head);
-            const int g = head & ~3;
-            const u32x4 x = *reinterpret_cast<const u32x4 *>(word_ptr(g));
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ring[((g + i) & (kRing - 1)) * ENVS] = x[i];
-            tail = g + 4;
-        }
+        if (head >= tail) refill_lane();   // the ring ran dry inside one step (a rejection streak)
         const uint32_t y = ring[(head & (kRing - 1)) * ENVS];
         ++head;
         return y;
     }
-    // word head + k, without advancing: valid for k < kPeek after a top_up (every lane then holds more
-    // than kRing / 4 words)
+    // word head + k, without advancing: valid for k <= kTopUp after a top_up
     __device__ __forceinline__ uint32_t peek(int k) const { return ring[((head + k) & (kRing - 1)) * ENVS]; }
     __device__ __forceinline__ double random() {
         const uint32_t a = next();
         return rand53(a, next());
     }
     __device__ __forceinline__ double uniform(double lo, double hi) { return lo + (hi - lo) * random(); }
-    // a draw whose value is discarded (a uniform: two words) only advances the stream
-    __device__ __forceinline__ void skip2() {
-        if (head + 2 <= tail) {
-            head += 2;
-        } else {
-            (void)next();
-            (void)next();
-        }
-    }
     __device__ __forceinline__ int randint(int low, int high) {   // exclusive high; one value: no draw
         if (high - 1 - low == 0) return low;
         uint32_t mask = (uint32_t)(high - 1 - low);
@@ -2626,8 +2621,9 @@ struct MtRingT {
         return (((cur0 + k) & 1) << 16) | (k + 1 < avail ? kMtNextReady : 0) | (head - k * kMtN);
     }
 };
-// One wavefront per workgroup; ENVS envs per wavefront (ref_day2_envs), the other lanes mirroring them.
-constexpr int kRefBlock = kWave;
+// Two wavefronts per workgroup over the same ENVS envs (lanes >= ENVS mirror them): wavefront 0 draws,
+// wavefront 1 writes the timeline.
+constexpr int kRefBlock = 2 * kWave;
 
 // The same day in two phases per charger, as generate_kernel draws a device day: (1) the charger's
 // vehicles, visiting only the steps that draw (a free step draws the arrival test, an arrival the
@@ -2636,9 +2632,15 @@ constexpr int kRefBlock = kWave;
 // by step.  Round 2's steps-major kernel executed the arrival path under a mask in nearly every (charger,
 // step) iteration of a wavefront; here a wavefront iterates once per draw step of its busiest lane
 // (about 5 of a charger's 24 steps draw).  The stream is consumed draw for draw.
+// Round 5: the phases run on two wavefronts of one workgroup.  The drawing wavefront (0) writes charger
+// c's list into LDS buffer c & 1 and meets the timeline wavefront (1) at one barrier per charger; the
+// timeline wavefront then writes charger c's timeline from that buffer while the drawing wavefront draws
+// charger c + 1 into the other one.  Round 4's single wavefront issued ~50 timeline stores per charger,
+// and on gfx9 stores count in vmcnt ahead of any later load, so the next charger's first ring refill
+// waited for all of them to complete (~0.8 us per charger) and the stores did not overlap the draws.
 constexpr int kRefVeh = 8;   // vehicles per charger-day (T / (4/dt + 1) + 1 <= 7 for every dt dividing 24 h) + sentinel
 // Phase 1 reads each draw step's words from the ring in two batches of LDS reads instead of one round
-// trip per word: after a top_up every lane still drawing holds more than kRing / 4 words, so the 10 words
+// trip per word: after a top_up every lane still drawing holds more than kTopUp words, so the 10 words
 // an arrival may need first (arrival test, SoC, the discarded uniform, four capacity candidates) and the
 // 6 it may need next (requested SoC, four departure candidates) are peeked without a bound check.  A
 // masked rejection (numpy's legacy bounded randint) takes the first of four candidates that passes; all
@@ -2655,193 +2657,223 @@ constexpr uint64_t kArrive53 = 0x13333333333334ull;
 __device__ __forceinline__ bool arrives(uint32_t wa, uint32_t wb) {
     return ((((uint64_t)(wa >> 5)) << 26) | (uint64_t)(wb >> 6)) >= kArrive53;
 }
+// LDS of ref_day2_kernel: the rings, then the two list buffers ([V][ENVS] each: entry, arrival SoC, and the
+// requested SoC with REQ)
+__host__ __device__ constexpr size_t ref_day2_list_bytes(bool req, int envs) {
+    return (size_t)kRefVeh * envs * (4 + 8 + (req ? 8 : 0));
+}
+__host__ __device__ constexpr size_t ref_day2_lds_bytes(bool req, int envs) {
+    return (size_t)kRing * envs * 4 + 2 * ref_day2_list_bytes(req, envs);
+}
 template <int TT, bool REQ, int ENVS>
 __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceState s, RefStreams rs, int64_t E,
                                                              int i4, int i10, int i1) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rd_lds[];
     uint32_t *rings = rd_lds;                                          // [kRing][ENVS]
-    uint32_t *s_veh = rings + kRing * ENVS;                         // [V][ENVS] ta | cap << 8 | dep << 16
-    double *s_soc = reinterpret_cast<double *>(s_veh + kRefVeh * ENVS);   // [V][ENVS] arrival SoC
-    double *s_req = s_soc + kRefVeh * ENVS;                          // [V][ENVS] requested SoC (REQ)
-    const int lane = threadIdx.x % ENVS;   // the env slot; lanes >= ENVS mirror it
+    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);   // 0 draws, 1 writes
+    const int lane = (int)threadIdx.x % ENVS;   // the env slot; lanes >= ENVS of either wavefront mirror it
     const int64_t e0 = (int64_t)blockIdx.x * ENVS;
     const bool live = e0 + lane < E && (int)threadIdx.x < ENVS;
     const int64_t e = e0 + lane < E ? e0 + lane : E - 1;   // past E: env E - 1's stream, nothing stored
-    const int32_t pos = rs.pos[e];
-    const int mti = pos & kMtPosMask;
-    MtRingT<ENVS> rng{rs.mt + (size_t)e * 2 * kMtN, rings + lane, (pos >> 16) & 1, mti, mti & ~3, mti, 2};
+    // the list buffer of charger c: entries ta | cap << W_CAP_SHIFT | dep << W_DEP_SHIFT, then arrival SoC, then
+    // requested SoC (REQ)
+    auto list_veh = [&](int c) {
+        return reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(rd_lds) + (size_t)kRing * ENVS * 4 +
+                                            (size_t)(c & 1) * ref_day2_list_bytes(REQ, ENVS));
+    };
+    auto list_soc = [&](int c) { return reinterpret_cast<double *>(list_veh(c) + kRefVeh * ENVS); };
+    auto list_req = [&](int c) { return list_soc(c) + kRefVeh * ENVS; };
     const int T = TT > 0 ? TT : p.T, n = p.n;
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;   // as generate_kernel
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
     const uint32_t el8 = (uint32_t)e * 8u;
     const size_t nE = (size_t)n * (size_t)E;
-    // diagnostic builds: stamps 0 / 1 the kernel's start and end, 2 / 3 the ticks in phase 1 / phase 2
+    // diagnostic builds: stamps 0 / 1 the drawing wavefront's start and end, 2 its ticks in phase 1 (7 its
+    // HW_ID); 3 the timeline wavefront's ticks in phase 2, 4 its end, 5 its HW_ID
     SNG_WSTAMP_DECL;
     SNG_WSTAMP(0);
+    MtRingT<ENVS> rng;
+    if (wv == 0) {
+        const int32_t pos = rs.pos[e];
+        rng.blk = rs.mt + (size_t)e * 2 * kMtN;
+        rng.ring = rings + lane;
+        rng.cur0 = (pos >> 16) & 1;
+        rng.start(pos & kMtPosMask);
+    }
     for (int c = 0; c < n; ++c) {
-        const uint32_t r4 = (uint32_t)c * (uint32_t)E * 4u, r8 = 2u * r4;
-        [[maybe_unused]] const unsigned long long t1_ = SNG_WNOW();
-        // phase 1: the charger's vehicles, one iteration per step that draws
-        int t = 0, nv = 0;
-        while (t < T) {
-            rng.top_up();   // ballots over the lanes still drawing: each then holds > kRing / 4 words
-            // the next kScan steps' arrival draws at once: the first that arrives, the free steps before
-            // it consumed together
-            uint32_t a[2 * kScan];
+        if (wv == 0) {
+            [[maybe_unused]] const unsigned long long t1_ = SNG_WNOW();
+            uint32_t *s_veh = list_veh(c);
+            double *s_soc = list_soc(c), *s_req = list_req(c);
+            // phase 1: the charger's vehicles, one iteration per step that draws
+            int t = 0, nv = 0;
+            while (t < T) {
+                rng.top_up();   // ballots over the lanes still drawing: each then holds > kTopUp words
+                // the next kScan steps' arrival draws at once: the first that arrives, the free steps before
+                // it consumed together
+                uint32_t a[2 * kScan];
 #pragma unroll
-            for (int k = 0; k < 2 * kScan; ++k) a[k] = rng.peek(k);
-            int j = kScan;
+                for (int k = 0; k < 2 * kScan; ++k) a[k] = rng.peek(k);
+                int j = kScan;
 #pragma unroll
-            for (int kk = kScan - 1; kk >= 0; --kk) j = arrives(a[2 * kk], a[2 * kk + 1]) ? kk : j;
-            const int skip = min(j, T - t);
-            rng.head += 2 * skip;
-            t += skip;
-            if (t < T && j < kScan) {   // an arrival at step t
-                uint32_t w[10];   // from the arrival draw: w[0], w[1] are it (not reread)
+                for (int kk = kScan - 1; kk >= 0; --kk) j = arrives(a[2 * kk], a[2 * kk + 1]) ? kk : j;
+                const int skip = min(j, T - t);
+                rng.head += 2 * skip;
+                t += skip;
+                if (t < T && j < kScan) {   // an arrival at step t
+                    uint32_t w[10];   // from the arrival draw: w[0], w[1] are it (not reread)
 #pragma unroll
-                for (int k = 2; k < 10; ++k) w[k] = rng.peek(k);
-                const double soc = 0.1 + (0.9 - 0.1) * rand53(w[2], w[3]);      // uniform(0.1, 0.9), :257-259
-                const double lo = soc <= 0.9 ? soc + 0.1 : 1.0;
-                // w[4], w[5]: the discarded uniform (:219)
-                uint32_t cap = 40u;
-                bool seq = false;   // the draws continue word by word (a rejection streak)
-                if (p.diff_caps) {   // randint(15, 120) (:267-269): mask 127, accept <= 104
-                    int k = 4;
-                    uint32_t cv = 0u;
-#pragma unroll
-                    for (int kk = 3; kk >= 0; --kk) {   // the first candidate that passes, without an index
-                        const uint32_t x = w[6 + kk] & 127u;
-                        k = (x <= 104u) ? kk : k;
-                        cv = (x <= 104u) ? x : cv;
-                    }
-                    if (k < 4) {
-                        cap = 15u + cv;
-                        rng.head += 7 + k;
-                    } else {
-                        rng.head += 10;
-                        cap = (uint32_t)rng.randint(15, 120);
-                        seq = true;
-                    }
-                } else {
-                    rng.head += 6;
-                }
-                double rq = 1.0;
-                const int high = min(t + i10, T + i1), low = t + i4;             // :271-279
-                int dep = low;
-                if (!seq) {
-                    uint32_t v[6];
-#pragma unroll
-                    for (int k = 0; k < 6; ++k) v[k] = rng.peek(k);
-                    constexpr int U = REQ ? 2 : 0;
-                    if (REQ) rq = lo + (1.0 - lo) * rand53(v[0], v[1]);       // uniform(lo, 1), :261-265
-                    int used = U;
-                    if (low < high && high - 1 - low > 0) {   // randint(low, high); one value draws nothing
-                        const uint32_t span = (uint32_t)(high - 1 - low);
-                        uint32_t mask = span;
-                        mask |= mask >> 1;
-                        mask |= mask >> 2;
-                        mask |= mask >> 4;
-                        mask |= mask >> 8;
-                        mask |= mask >> 16;
+                    for (int k = 2; k < 10; ++k) w[k] = rng.peek(k);
+                    const double soc = 0.1 + (0.9 - 0.1) * rand53(w[2], w[3]);      // uniform(0.1, 0.9), :257-259
+                    const double lo = soc <= 0.9 ? soc + 0.1 : 1.0;
+                    // w[4], w[5]: the discarded uniform (:219)
+                    uint32_t cap = 40u;
+                    bool seq = false;   // the draws continue word by word (a rejection streak)
+                    if (p.diff_caps) {   // randint(15, 120) (:267-269): mask 127, accept <= 104
                         int k = 4;
-                        uint32_t dv = 0u;
+                        uint32_t cv = 0u;
 #pragma unroll
-                        for (int kk = 3; kk >= 0; --kk) {
-                            const uint32_t x = v[U + kk] & mask;
-                            k = (x <= span) ? kk : k;
-                            dv = (x <= span) ? x : dv;
+                        for (int kk = 3; kk >= 0; --kk) {   // the first candidate that passes, without an index
+                            const uint32_t x = w[6 + kk] & 127u;
+                            k = (x <= 104u) ? kk : k;
+                            cv = (x <= 104u) ? x : cv;
                         }
                         if (k < 4) {
-                            dep = low + (int)dv;
-                            used += k + 1;
+                            cap = 15u + cv;
+                            rng.head += 7 + k;
                         } else {
-                            rng.head += U + 4;
-                            used = 0;
-                            uint32_t x;
-                            while ((x = (rng.next() & mask)) > span) {
-                            }
-                            dep = low + (int)x;
+                            rng.head += 10;
+                            cap = (uint32_t)rng.randint(15, 120);
+                            seq = true;
                         }
+                    } else {
+                        rng.head += 6;
                     }
-                    rng.head += used;
-                } else {
-                    rq = REQ ? rng.uniform(lo, 1.0) : 1.0;
-                    dep = (low >= high) ? low : rng.randint(low, high);
-                }
-                const int vi = nv < kRefVeh - 1 ? nv : kRefVeh - 2;   // at most 7 (see kRefVeh)
-                s_veh[vi * ENVS + lane] = (uint32_t)t | (cap << W_CAP_SHIFT) | ((uint32_t)dep << W_DEP_SHIFT);
-                s_soc[vi * ENVS + lane] = soc;
-                if (REQ) s_req[vi * ENVS + lane] = rq;
-                nv = vi + 1;
-                t = dep + 1;   // occupied until dep - 1; the departure step is empty and draws nothing
-            }
-        }
-        s_veh[nv * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);   // sentinel: never arrives
-        s_veh[(nv + 1 < kRefVeh ? nv + 1 : nv) * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);
-        SNG_WACC(2, t1_);
-        [[maybe_unused]] const unsigned long long t2_ = SNG_WNOW();
-        // phase 2: the timeline (encode_day, sng_api.cpp): cur = the vehicle of step t until step t has
-        // passed its departure step, nxt the one after it (read a step ahead); a stay of zero steps
-        // (dep == arrival, possible when 4/dt < 1) still marks its arrival step STATIC, as the host
-        // encoder's arrival list does
-        int v = 0;
-        uint32_t cur = s_veh[lane], nxt = s_veh[ENVS + lane];
-        double soc_cur = s_soc[lane], soc_nxt = s_soc[ENVS + lane];
-        double req_cur = REQ ? s_req[lane] : 1.0, req_nxt = REQ ? s_req[ENVS + lane] : 1.0;
-        bool prev_occ = false;
-        uint32_t prev_rem = 0u;
-        double prev_req = 0.0;
+                    double rq = 1.0;
+                    const int high = min(t + i10, T + i1), low = t + i4;             // :271-279
+                    int dep = low;
+                    if (!seq) {
+                        uint32_t v[6];
 #pragma unroll
-        for (int tt = 0; tt < T; ++tt) {
-            const uint32_t ta = cur & 0xffu, dep = cur >> W_DEP_SHIFT;
-            const bool adv = (uint32_t)(tt + 1) > dep;   // step t + 1 belongs to the next vehicle
-            const int vr = v + 2 < kRefVeh ? v + 2 : kRefVeh - 1;
-            const uint32_t nn = s_veh[vr * ENVS + lane];   // list[v + 2], for when nxt becomes current
-            const double soc_nn = s_soc[vr * ENVS + lane];
-            const double req_nn = REQ ? s_req[vr * ENVS + lane] : 1.0;
-            const bool occ = (uint32_t)tt >= ta && (uint32_t)tt < dep;
-            const bool arrived = (uint32_t)tt == ta;
-            const bool running = !arrived && prev_occ;
-            const uint32_t rem = occ ? dep - (uint32_t)tt : 0u;
-            const bool pen = prev_rem - pen_lo <= pen_span;   // prev_rem = 0: empty at t-1
-            const size_t plane = (size_t)tt * nE;
-            // every lane stores: a lane that is not live mirrors a live one (the same env's stream, so
-            // the same values to the same addresses), and straight-line stores let the compiler count
-            // them in vmcnt instead of draining them before the next refill's words are read
-            {
-                // plain global stores (a uniform plane pointer + the env): one buffer descriptor per plane
-                // would not fit the SGPRs of the unrolled walk
-                const size_t row = plane + (size_t)c * (size_t)E;
-                s.word[row + (size_t)e] = pack_word(occ, !running, pen, occ ? (cur >> W_CAP_SHIFT) & 0xffu : 0u, rem);
-                s.aux[row + (size_t)e] = (occ && !running) ? soc_cur : 0.0;
-                if (REQ && tt > 0) s.req[row + (size_t)e] = prev_req;   // Requested_SOC[c, t-1]
+                        for (int k = 0; k < 6; ++k) v[k] = rng.peek(k);
+                        constexpr int U = REQ ? 2 : 0;
+                        if (REQ) rq = lo + (1.0 - lo) * rand53(v[0], v[1]);       // uniform(lo, 1), :261-265
+                        int used = U;
+                        if (low < high && high - 1 - low > 0) {   // randint(low, high); one value draws nothing
+                            const uint32_t span = (uint32_t)(high - 1 - low);
+                            uint32_t mask = span;
+                            mask |= mask >> 1;
+                            mask |= mask >> 2;
+                            mask |= mask >> 4;
+                            mask |= mask >> 8;
+                            mask |= mask >> 16;
+                            int k = 4;
+                            uint32_t dv = 0u;
+#pragma unroll
+                            for (int kk = 3; kk >= 0; --kk) {
+                                const uint32_t x = v[U + kk] & mask;
+                                k = (x <= span) ? kk : k;
+                                dv = (x <= span) ? x : dv;
+                            }
+                            if (k < 4) {
+                                dep = low + (int)dv;
+                                used += k + 1;
+                            } else {
+                                rng.head += U + 4;
+                                used = 0;
+                                uint32_t x;
+                                while ((x = (rng.next() & mask)) > span) {
+                                }
+                                dep = low + (int)x;
+                            }
+                        }
+                        rng.head += used;
+                    } else {
+                        rq = REQ ? rng.uniform(lo, 1.0) : 1.0;
+                        dep = (low >= high) ? low : rng.randint(low, high);
+                    }
+                    const int vi = nv < kRefVeh - 1 ? nv : kRefVeh - 2;   // at most 7 (see kRefVeh)
+                    s_veh[vi * ENVS + lane] = (uint32_t)t | (cap << W_CAP_SHIFT) | ((uint32_t)dep << W_DEP_SHIFT);
+                    s_soc[vi * ENVS + lane] = soc;
+                    if (REQ) s_req[vi * ENVS + lane] = rq;
+                    nv = vi + 1;
+                    t = dep + 1;   // occupied until dep - 1; the departure step is empty and draws nothing
+                }
             }
-            prev_occ = occ;
-            prev_rem = rem;
-            prev_req = occ ? req_cur : 0.0;
-            v += adv ? 1 : 0;
-            cur = adv ? nxt : cur;
-            soc_cur = adv ? soc_nxt : soc_cur;
-            req_cur = adv ? req_nxt : req_cur;
-            nxt = adv ? nn : nxt;
-            soc_nxt = adv ? soc_nn : soc_nxt;
-            req_nxt = adv ? req_nn : req_nxt;
+            s_veh[nv * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);   // sentinel: never arrives
+            s_veh[(nv + 1 < kRefVeh ? nv + 1 : nv) * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);
+            SNG_WACC(2, t1_);
         }
-        if (REQ) bst(s.req, el8, prev_req, r8);   // slot 0: Requested_SOC[c, T-1]
-        SNG_WACC(3, t2_);
+        __syncthreads();   // charger c's list is in buffer c & 1; the timeline wavefront is done with c - 1's
+        if (wv == 1) {
+            [[maybe_unused]] const unsigned long long t2_ = SNG_WNOW();
+            const uint32_t *s_veh = list_veh(c);
+            const double *s_soc = list_soc(c), *s_req = list_req(c);
+            // phase 2: the timeline (encode_day, sng_api.cpp): cur = the vehicle of step t until step t has
+            // passed its departure step, nxt the one after it (read a step ahead); a stay of zero steps
+            // (dep == arrival, possible when 4/dt < 1) still marks its arrival step STATIC, as the host
+            // encoder's arrival list does
+            int v = 0;
+            uint32_t cur = s_veh[lane], nxt = s_veh[ENVS + lane];
+            double soc_cur = s_soc[lane], soc_nxt = s_soc[ENVS + lane];
+            double req_cur = REQ ? s_req[lane] : 1.0, req_nxt = REQ ? s_req[ENVS + lane] : 1.0;
+            bool prev_occ = false;
+            uint32_t prev_rem = 0u;
+            double prev_req = 0.0;
+#pragma unroll
+            for (int tt = 0; tt < T; ++tt) {
+                const uint32_t ta = cur & 0xffu, dep = cur >> W_DEP_SHIFT;
+                const bool adv = (uint32_t)(tt + 1) > dep;   // step t + 1 belongs to the next vehicle
+                const int vr = v + 2 < kRefVeh ? v + 2 : kRefVeh - 1;
+                const uint32_t nn = s_veh[vr * ENVS + lane];   // list[v + 2], for when nxt becomes current
+                const double soc_nn = s_soc[vr * ENVS + lane];
+                const double req_nn = REQ ? s_req[vr * ENVS + lane] : 1.0;
+                const bool occ = (uint32_t)tt >= ta && (uint32_t)tt < dep;
+                const bool arrived = (uint32_t)tt == ta;
+                const bool running = !arrived && prev_occ;
+                const uint32_t rem = occ ? dep - (uint32_t)tt : 0u;
+                const bool pen = prev_rem - pen_lo <= pen_span;   // prev_rem = 0: empty at t-1
+                const size_t plane = (size_t)tt * nE;
+                // every lane stores: a lane that is not live mirrors a live one (the same env's stream, so
+                // the same values to the same addresses)
+                {
+                    // plain global stores (a uniform plane pointer + the env): one buffer descriptor per plane
+                    // would not fit the SGPRs of the unrolled walk
+                    const size_t row = plane + (size_t)c * (size_t)E;
+                    s.word[row + (size_t)e] = pack_word(occ, !running, pen, occ ? (cur >> W_CAP_SHIFT) & 0xffu : 0u, rem);
+                    s.aux[row + (size_t)e] = (occ && !running) ? soc_cur : 0.0;
+                    if (REQ && tt > 0) s.req[row + (size_t)e] = prev_req;   // Requested_SOC[c, t-1]
+                }
+                prev_occ = occ;
+                prev_rem = rem;
+                prev_req = occ ? req_cur : 0.0;
+                v += adv ? 1 : 0;
+                cur = adv ? nxt : cur;
+                soc_cur = adv ? soc_nxt : soc_cur;
+                req_cur = adv ? req_nxt : req_cur;
+                nxt = adv ? nn : nxt;
+                soc_nxt = adv ? soc_nn : soc_nxt;
+                req_nxt = adv ? req_nn : req_nxt;
+            }
+            if (REQ) bst(s.req, el8, prev_req, (uint32_t)c * (uint32_t)E * 8u);   // slot 0: Requested_SOC[c, T-1]
+            SNG_WACC(3, t2_);
+        }
     }
-    if (live) rs.pos[e] = rng.position();
-    SNG_WSTAMP(1);
-    SNG_WSTAMP_FLUSH(stamp_, 4);
+    if (wv == 0) {
+        if (live) rs.pos[e] = rng.position();
+        SNG_WSTAMP(1);
+        SNG_WSTAMP_FLUSH(stamp_, 3);
+    } else {
+        SNG_WSTAMP(4);
+        SNG_WSTAMP_PUT(3, stamp_[3], kWave);
+        SNG_WSTAMP_PUT(4, stamp_[4], kWave);
+        SNG_WSTAMP_PUT(5, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4), kWave);
+    }
 }
 
-__host__ __device__ constexpr size_t ref_day2_lds_bytes(bool req, int envs) {
-    return (size_t)kRing * envs * 4 + (size_t)kRefVeh * envs * (4 + 8 + (req ? 8 : 0));
-}
-
-// Envs per wavefront of ref_day2_kernel: each wavefront's day is one serial chain (an env's stream is
-// consumed charger after charger), so small populations spread over more, thinner wavefronts.
+// Envs per workgroup of ref_day2_kernel: each drawing wavefront's day is one serial chain (an env's stream
+// is consumed charger after charger), so small populations spread over more, thinner workgroups.
 static int ref_day2_envs(int64_t E) {
     return E >= 65536 ? 64 : E >= 16384 ? 32 : E >= 4096 ? 16 : 8;
 }

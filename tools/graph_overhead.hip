@@ -24,6 +24,7 @@
 typedef float v4f __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(64) void k_empty(float *) {}
+__global__ __launch_bounds__(1024) void k_empty_wide(float *) {}
 __global__ __launch_bounds__(64) void k_store(v4f *out) {
     const size_t i = (size_t)blockIdx.x * 64 + threadIdx.x;
     __builtin_nontemporal_store(v4f{1.f, 2.f, 3.f, 4.f}, out + i);
@@ -86,6 +87,18 @@ int main() {
     CK(hipMalloc(&in, nr * 16));
     CK(hipMalloc(&out, n * 16));
     CK(hipMemset(in, 0, nr * 16));
+    // the boundary's fixed part against its per-workgroup part: empty kernels of other grids
+    const int grids[][2] = {{1, 64}, {256, 64}, {512, 64}, {1024, 64}, {4096, 64}, {512, 256}, {256, 512}, {2048, 256}};
+    for (const auto &g : grids) {
+        char name[32];
+        snprintf(name, sizeof name, "empty%dx%d", g[0], g[1]);
+        measure(name, [&](hipStream_t s) {
+            if (g[1] == 64)
+                hipLaunchKernelGGL(k_empty, dim3(g[0]), dim3(g[1]), 0, s, (float *)out);
+            else
+                hipLaunchKernelGGL(k_empty_wide, dim3(g[0]), dim3(g[1]), 0, s, (float *)out);
+        });
+    }
     for (int rep = 0; rep < 2; ++rep) {
         measure("empty", [&](hipStream_t s) { hipLaunchKernelGGL(k_empty, dim3(2048), dim3(64), 0, s, (float *)out); });
         measure("store", [&](hipStream_t s) { hipLaunchKernelGGL(k_store, dim3(2048), dim3(64), 0, s, out); });

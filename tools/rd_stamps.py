@@ -3,10 +3,12 @@
     make -C tools/diag stamps
     SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng_stamps.so python tools/rd_stamps.py [--envs 65536]
 
-Per wavefront (64 envs): stamp 0 its start, stamp 1 its end, and the s_memrealtime ticks (10 ns) spent in
-phase 1 (the vehicles' draws, ring refills included) and phase 2 (the timeline walk and its stores) summed
-over the chargers.  The stamps take no wait of their own, so a wait for earlier stores shows up where the
-program next waits on memory (a refill of the next charger's phase 1).
+Per workgroup (64 envs, two wavefronts since round 5): stamp 0 its start, 1 the drawing wavefront's end,
+4 the timeline wavefront's end, and the s_memrealtime ticks (10 ns) the drawing wavefront spent in phase 1
+(the vehicles' draws, ring refills included, 2) and the timeline wavefront in phase 2 (the walk and its
+stores, 3), summed over the chargers; 7 and 5 the two wavefronts' HW_ID (CU, SIMD, wave slot), so the table
+shows how often both sit on one SIMD and how often two drawing wavefronts share one.  The stamps take no
+wait of their own.
 """
 import argparse
 import ctypes
@@ -36,7 +38,7 @@ def main():
     blocks = (E + 63) // 64
     buf = torch.zeros(max(blocks, 4096) * 8, dtype=torch.int64, device=venv.device)
     acts = torch.rand((24, E, venv.act_dim), device=venv.device)
-    rows = []
+    rows, ids = [], []
     for day in range(args.days):
         torch.cuda.synchronize()
         buf.zero_()
@@ -45,21 +47,33 @@ def main():
         torch.cuda.synchronize()
         assert setter(ctypes.c_void_p(0)) == 0
         if day > 0:
-            rows.append(buf.view(-1, 8)[:blocks, :4].cpu().numpy().astype(np.float64) * 10.0)   # ns
+            raw = buf.view(-1, 8)[:blocks].cpu().numpy()
+            rows.append(raw[:, :5].astype(np.float64) * 10.0)   # ns
+            ids.append(raw[:, [7, 5]])
         for t in range(24):
             venv.step_tensors(acts[t])
     venv.close()
-    st = np.stack(rows)   # [days, waves, 4]
-    span = st[..., 1].max(axis=1) - st[..., 0].min(axis=1)
-    own = st[..., 1] - st[..., 0]
+    st = np.stack(rows)   # [days, workgroups, 6]
+    end = np.maximum(st[..., 1], st[..., 4])
+    span = end.max(axis=1) - st[..., 0].min(axis=1)
+    own = end - st[..., 0]
     q = lambda x: f"med {np.median(x) / 1e3:7.2f}  p10 {np.percentile(x, 10) / 1e3:7.2f}  p90 {np.percentile(x, 90) / 1e3:7.2f} us"
-    print(f"ref_day2_kernel, {E} envs, {blocks} wavefronts, {args.days - 1} days")
+    print(f"ref_day2_kernel, {E} envs, {blocks} workgroups, {args.days - 1} days")
     print("kernel span (first start to last end) ", q(span))
-    print("wavefront start (rel. first)         ", q(st[..., 0] - st[..., 0].min(axis=1, keepdims=True)))
-    print("wavefront own time                   ", q(own))
-    print("  phase 1 (draws, refills)           ", q(st[..., 2]))
-    print("  phase 2 (timeline walk, stores)    ", q(st[..., 3]))
-    print("  rest (setup, position store)       ", q(own - st[..., 2] - st[..., 3]))
+    print("workgroup start (rel. first)         ", q(st[..., 0] - st[..., 0].min(axis=1, keepdims=True)))
+    print("workgroup own time                   ", q(own))
+    print("  drawing wavefront: phase 1 (draws, refills)   ", q(st[..., 2]))
+    print("  timeline wavefront: phase 2 (walk, stores)    ", q(st[..., 3]))
+    print("  timeline wavefront ends after the drawing one ", q(st[..., 4] - st[..., 1]))
+    # HW_ID: wave slot bits 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13 (gfx9); XCC is not in it, so the CU key
+    # here merges the same CU number of the eight XCDs
+    hw = ids[-1].astype(np.int64)
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 0xffff
+    same = np.mean((cu[:, 0] == cu[:, 1]) & (simd[:, 0] == simd[:, 1]))
+    print(f"last day: both wavefronts of a workgroup on one SIMD {same:.1%}; "
+          f"SIMDs of the drawing wavefronts {np.bincount(simd[:, 0], minlength=4).tolist()}, "
+          f"of the timeline wavefronts {np.bincount(simd[:, 1], minlength=4).tolist()}")
 
 
 if __name__ == "__main__":

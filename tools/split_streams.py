@@ -1,5 +1,5 @@
 """Experiment: the bench day (65,536 envs x 10 chargers) as S independent env slices, each a
-hipGraph replayed on its own HIP stream, so one slice's compute phase overlaps another's
+hipGraph of D days replayed on its own HIP stream, so one slice's compute phase overlaps another's
 memory phase.  Prints ms/day and env-steps/s per S.
 
     python tools/split_streams.py [S ...]
@@ -16,7 +16,7 @@ import torch  # noqa: E402
 from smart_nanogrid_gym import EpisodeGraph, SmartNanogridVecEnv  # noqa: E402
 
 
-def run(S, E=65536, N=10, days=30, warm=3):
+def run(S, E=65536, N=10, days=5, warm=2, D=20):
     kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
               vehicle_uncharged_penalty_mode="sparse", pv_system_available_in_model=True,
               battery_system_available_in_model=True)
@@ -31,7 +31,7 @@ def run(S, E=65536, N=10, days=30, warm=3):
         acts = (low + (high - low) * torch.rand((v.timesteps, per, v.act_dim), generator=g, device=dev)).contiguous()
         v._info.flags = None
         venvs.append(v)
-        graphs.append(EpisodeGraph(v, acts, with_reset=True))
+        graphs.append(EpisodeGraph(v, acts, with_reset=True, days=D))
         streams.append(torch.cuda.Stream(dev))
     def day():
         for g, s in zip(graphs, streams):
@@ -43,7 +43,7 @@ def run(S, E=65536, N=10, days=30, warm=3):
     for _ in range(days):
         day()
     torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / days
+    dt = (time.perf_counter() - t0) / (days * D)
     print(f"S={S}: {dt * 1e3:.4f} ms/day  {E * 24 / dt:.4e} env-steps/s", flush=True)
     for g in graphs:
         g.close()
