@@ -27,10 +27,11 @@ __device__ unsigned long long *g_stamps;
             g_stamps[(size_t)blockIdx.x * 8 + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 4);          \
         }                                                                                              \
     } while (0)
-// one slot written by thread tid of the workgroup (a second wavefront's own stamps)
-#define SNG_WSTAMP_PUT(slot, v, tid)                                                                   \
-    do {                                                                                               \
-        if ((int)threadIdx.x == (tid) && g_stamps) g_stamps[(size_t)blockIdx.x * 8 + (slot)] = (v);   \
+// one slot of record idx (8 slots per record) written by thread tid of the workgroup: a kernel with several
+// records per workgroup (ref_day2_kernel: one per group of envs) or several wavefronts per record
+#define SNG_WSTAMP_PUT(slot, v, idx, tid)                                                        \
+    do {                                                                                         \
+        if ((int)threadIdx.x == (tid) && g_stamps) g_stamps[(size_t)(idx) * 8 + (slot)] = (v);   \
     } while (0)
 #define SNG_DIAG_SET_STAMPS                                                                         \
     extern "C" int sng_debug_set_stamps(unsigned long long *dev_ptr) {                              \
@@ -44,8 +45,8 @@ __device__ unsigned long long *g_stamps;
 #define SNG_WSTAMP_FLUSH(arr, n) \
     do {                         \
     } while (0)
-#define SNG_WSTAMP_PUT(slot, v, tid) \
-    do {                             \
+#define SNG_WSTAMP_PUT(slot, v, idx, tid) \
+    do {                                  \
     } while (0)
 #define SNG_WNOW() 0ull
 #define SNG_WACC(k, t0) \

@@ -2621,9 +2621,15 @@ struct MtRingT {
         return (((cur0 + k) & 1) << 16) | (k + 1 < avail ? kMtNextReady : 0) | (head - k * kMtN);
     }
 };
-// Two wavefronts per workgroup over the same ENVS envs (lanes >= ENVS mirror them): wavefront 0 draws,
-// wavefront 1 writes the timeline.
-constexpr int kRefBlock = 2 * kWave;
+// kRefGroups groups of ENVS envs per workgroup (lanes >= ENVS mirror them), each with a drawing wavefront
+// (wavefront g) and a timeline wavefront (wavefront kRefGroups + g).  One group per workgroup: the
+// dispatcher then puts two drawing wavefronts (and a timeline one) on ~96 of the 1,024 SIMDs, and their
+// workgroups set the kernel's span (84 us against a median of 68 us).  Four groups (a workgroup of 8
+// wavefronts fills one CU, wavefronts w and w + 4 on one SIMD) placed every drawing wavefront beside a
+// timeline one, but the workgroup's barriers then couple four drawing wavefronts, and the span stayed at
+// 85 us (A/B, profiles/r05_ab_refday_two_wavefronts.txt).
+constexpr int kRefGroups = 1;
+constexpr int kRefBlock = 2 * kRefGroups * kWave;
 
 // The same day in two phases per charger, as generate_kernel draws a device day: (1) the charger's
 // vehicles, visiting only the steps that draw (a free step draws the arrival test, an arrival the
@@ -2657,59 +2663,80 @@ constexpr uint64_t kArrive53 = 0x13333333333334ull;
 __device__ __forceinline__ bool arrives(uint32_t wa, uint32_t wb) {
     return ((((uint64_t)(wa >> 5)) << 26) | (uint64_t)(wb >> 6)) >= kArrive53;
 }
-// LDS of ref_day2_kernel: the rings, then the two list buffers ([V][ENVS] each: entry, arrival SoC, and the
+// Vehicle-list buffers of ref_day2_kernel: charger c's list is in buffer c mod D.  The drawing wavefront's
+// lanes do not wait for each other at the end of a charger: a lane that has drawn charger c's vehicles goes
+// on to charger c + 1 while the wavefront's slowest lane still draws charger c (D = 3: one charger ahead;
+// the timeline wavefront reads the buffer of charger c - 1 meanwhile).  A wavefront then iterates about as
+// often as its busiest lane over the whole station (~41 times a day, simulated) instead of the sum over the
+// chargers of each one's busiest lane (~51).  With the requested-SoC lists (REQ) two buffers fit the LDS
+// of four workgroups per CU, and the lanes keep in step charger by charger.
+__host__ __device__ constexpr int ref_day2_lists(bool req) { return req ? 2 : 3; }
+// LDS of ref_day2_kernel: the rings, then the list buffers ([V][ENVS] each: entry, arrival SoC, and the
 // requested SoC with REQ)
 __host__ __device__ constexpr size_t ref_day2_list_bytes(bool req, int envs) {
     return (size_t)kRefVeh * envs * (4 + 8 + (req ? 8 : 0));
 }
-__host__ __device__ constexpr size_t ref_day2_lds_bytes(bool req, int envs) {
-    return (size_t)kRing * envs * 4 + 2 * ref_day2_list_bytes(req, envs);
+__host__ __device__ constexpr size_t ref_day2_group_bytes(bool req, int envs) {
+    return (size_t)kRing * envs * 4 + (size_t)ref_day2_lists(req) * ref_day2_list_bytes(req, envs);
 }
+__host__ __device__ constexpr size_t ref_day2_lds_bytes(bool req, int envs) {
+    return (size_t)kRefGroups * ref_day2_group_bytes(req, envs);
+}
+static_assert(ref_day2_lds_bytes(true, 64) <= 160 * 1024 && ref_day2_lds_bytes(false, 64) <= 160 * 1024,
+              "a ref_day2_kernel workgroup fits one CU's LDS");
 template <int TT, bool REQ, int ENVS>
-__global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceState s, RefStreams rs, int64_t E,
+__global__ __launch_bounds__(kRefBlock) __attribute__((amdgpu_waves_per_eu(2))) void ref_day2_kernel(Params p, DeviceState s, RefStreams rs, int64_t E,
                                                              int i4, int i10, int i1) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rd_lds[];
-    uint32_t *rings = rd_lds;                                          // [kRing][ENVS]
-    const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);   // 0 draws, 1 writes
-    const int lane = (int)threadIdx.x % ENVS;   // the env slot; lanes >= ENVS of either wavefront mirror it
-    const int64_t e0 = (int64_t)blockIdx.x * ENVS;
-    const bool live = e0 + lane < E && (int)threadIdx.x < ENVS;
+    const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
+    const int wv = w / kRefGroups, g = w % kRefGroups;   // wv 0 draws, 1 writes group g's timeline
+    const int wl = (int)threadIdx.x % kWave;
+    const int lane = wl % ENVS;   // the env slot; lanes >= ENVS of either wavefront mirror it
+    const int rec = (int)blockIdx.x * kRefGroups + g;   // the group's index (diagnostic stamps)
+    const int64_t e0 = (int64_t)rec * ENVS;
+    const bool live = e0 + lane < E && wl < ENVS;
     const int64_t e = e0 + lane < E ? e0 + lane : E - 1;   // past E: env E - 1's stream, nothing stored
-    // the list buffer of charger c: entries ta | cap << W_CAP_SHIFT | dep << W_DEP_SHIFT, then arrival SoC, then
-    // requested SoC (REQ)
-    auto list_veh = [&](int c) {
-        return reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(rd_lds) + (size_t)kRing * ENVS * 4 +
-                                            (size_t)(c & 1) * ref_day2_list_bytes(REQ, ENVS));
+    // the group's LDS: its ring [kRing][ENVS], then its list buffers
+    uint32_t *glds = rd_lds + (size_t)g * ref_day2_group_bytes(REQ, ENVS) / 4;
+    uint32_t *rings = glds;
+    // list buffer b (charger c's is c mod D): entries ta | cap << W_CAP_SHIFT | dep << W_DEP_SHIFT, then arrival
+    // SoC, then requested SoC (REQ)
+    constexpr int D = ref_day2_lists(REQ);
+    auto list_veh = [&](int b) {
+        return reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(glds) + (size_t)kRing * ENVS * 4 +
+                                            (size_t)b * ref_day2_list_bytes(REQ, ENVS));
     };
-    auto list_soc = [&](int c) { return reinterpret_cast<double *>(list_veh(c) + kRefVeh * ENVS); };
-    auto list_req = [&](int c) { return list_soc(c) + kRefVeh * ENVS; };
+    auto list_soc = [&](int b) { return reinterpret_cast<double *>(list_veh(b) + kRefVeh * ENVS); };
+    auto list_req = [&](int b) { return list_soc(b) + kRefVeh * ENVS; };
     const int T = TT > 0 ? TT : p.T, n = p.n;
     const uint32_t pen_lo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256u : 1u;   // as generate_kernel
     const uint32_t pen_span = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2u
                               : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254u : 0u;
     const uint32_t el8 = (uint32_t)e * 8u;
     const size_t nE = (size_t)n * (size_t)E;
-    // diagnostic builds: stamps 0 / 1 the drawing wavefront's start and end, 2 its ticks in phase 1 (7 its
-    // HW_ID); 3 the timeline wavefront's ticks in phase 2, 4 its end, 5 its HW_ID
+    // diagnostic builds: stamps 0 / 1 the drawing wavefront's start and end, 2 its ticks in phase 1 (6, 7 its
+    // XCC id and HW_ID); 3 the timeline wavefront's ticks in phase 2, 4 its end, 5 its HW_ID | XCC id << 32
     SNG_WSTAMP_DECL;
     SNG_WSTAMP(0);
-    MtRingT<ENVS> rng;
     if (wv == 0) {
+        [[maybe_unused]] const unsigned long long t1_ = SNG_WNOW();
+        MtRingT<ENVS> rng;
         const int32_t pos = rs.pos[e];
         rng.blk = rs.mt + (size_t)e * 2 * kMtN;
         rng.ring = rings + lane;
         rng.cur0 = (pos >> 16) & 1;
         rng.start(pos & kMtPosMask);
-    }
-    for (int c = 0; c < n; ++c) {
-        if (wv == 0) {
-            [[maybe_unused]] const unsigned long long t1_ = SNG_WNOW();
-            uint32_t *s_veh = list_veh(c);
-            double *s_soc = list_soc(c), *s_req = list_req(c);
-            // phase 1: the charger's vehicles, one iteration per step that draws
-            int t = 0, nv = 0;
-            while (t < T) {
-                rng.top_up();   // ballots over the lanes still drawing: each then holds > kTopUp words
+        // phase 1: every lane draws its chargers' vehicles, one iteration per step that draws, charger after
+        // charger; the wavefront meets the timeline wavefronts once all its lanes are past charger k (barrier
+        // k + 1: the workgroup's, so the groups' drawing wavefronts meet there too), and a lane draws charger c
+        // only while c <= k + D - 2 (its buffer is free)
+        int c = 0, cb = 0, t = 0, nv = 0;   // the lane's charger, its buffer (c mod D), step, vehicles so far
+        int kb = 0;                          // barriers passed (wave-uniform): k above
+        uint32_t *s_veh = list_veh(0);
+        double *s_soc = list_soc(0), *s_req = list_req(0);
+        while (kb < n) {
+            if (c < n && c <= kb + D - 2) {
+                rng.top_up();   // ballots over the lanes drawing: each then holds > kTopUp words
                 // the next kScan steps' arrival draws at once: the first that arrives, the free steps before
                 // it consumed together
                 uint32_t a[2 * kScan];
@@ -2800,16 +2827,32 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
                     nv = vi + 1;
                     t = dep + 1;   // occupied until dep - 1; the departure step is empty and draws nothing
                 }
+                if (t >= T) {   // the charger's list is complete: the sentinel, then the next charger
+                    s_veh[nv * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);   // never arrives
+                    s_veh[(nv + 1 < kRefVeh ? nv + 1 : nv) * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);
+                    ++c;
+                    cb = cb + 1 == D ? 0 : cb + 1;
+                    t = 0;
+                    nv = 0;
+                    s_veh = list_veh(cb);
+                    s_soc = list_soc(cb);
+                    s_req = list_req(cb);
+                }
             }
-            s_veh[nv * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);   // sentinel: never arrives
-            s_veh[(nv + 1 < kRefVeh ? nv + 1 : nv) * ENVS + lane] = 0xffu | (0xffu << W_DEP_SHIFT);
-            SNG_WACC(2, t1_);
+            // every lane past charger k: its list is complete, and the timeline wavefront may take it
+            while (kb < n && __builtin_amdgcn_ballot_w64(c <= kb) == 0) {
+                __syncthreads();   // barrier k + 1 (the timeline wavefront's of charger k)
+                ++kb;
+            }
         }
-        __syncthreads();   // charger c's list is in buffer c & 1; the timeline wavefront is done with c - 1's
-        if (wv == 1) {
+        SNG_WACC(2, t1_);
+        if (live) rs.pos[e] = rng.position();
+    } else {
+        for (int c = 0; c < n; ++c) {
+            __syncthreads();   // charger c's list is complete, in buffer c mod D
             [[maybe_unused]] const unsigned long long t2_ = SNG_WNOW();
-            const uint32_t *s_veh = list_veh(c);
-            const double *s_soc = list_soc(c), *s_req = list_req(c);
+            const uint32_t *s_veh = list_veh(c % D);
+            const double *s_soc = list_soc(c % D), *s_req = list_req(c % D);
             // phase 2: the timeline (encode_day, sng_api.cpp): cur = the vehicle of step t until step t has
             // passed its departure step, nxt the one after it (read a step ahead); a stay of zero steps
             // (dep == arrival, possible when 4/dt < 1) still marks its arrival step STATIC, as the host
@@ -2860,15 +2903,20 @@ __global__ __launch_bounds__(kRefBlock) void ref_day2_kernel(Params p, DeviceSta
             SNG_WACC(3, t2_);
         }
     }
+    const int t0 = w * kWave;   // the wavefront's first thread writes its stamps
     if (wv == 0) {
-        if (live) rs.pos[e] = rng.position();
         SNG_WSTAMP(1);
-        SNG_WSTAMP_FLUSH(stamp_, 3);
+        SNG_WSTAMP_PUT(0, stamp_[0], rec, t0);
+        SNG_WSTAMP_PUT(1, stamp_[1], rec, t0);
+        SNG_WSTAMP_PUT(2, stamp_[2], rec, t0);
+        SNG_WSTAMP_PUT(6, (unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20), rec, t0);
+        SNG_WSTAMP_PUT(7, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4), rec, t0);
     } else {
         SNG_WSTAMP(4);
-        SNG_WSTAMP_PUT(3, stamp_[3], kWave);
-        SNG_WSTAMP_PUT(4, stamp_[4], kWave);
-        SNG_WSTAMP_PUT(5, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4), kWave);
+        SNG_WSTAMP_PUT(3, stamp_[3], rec, t0);
+        SNG_WSTAMP_PUT(4, stamp_[4], rec, t0);
+        SNG_WSTAMP_PUT(5, (unsigned long long)__builtin_amdgcn_s_getreg((31 << 11) | 4) |
+                              ((unsigned long long)__builtin_amdgcn_s_getreg((3 << 11) | 20) << 32), rec, t0);
     }
 }
 
@@ -2878,17 +2926,30 @@ static int ref_day2_envs(int64_t E) {
     return E >= 65536 ? 64 : E >= 16384 ? 32 : E >= 4096 ? 16 : 8;
 }
 
+// more than 64 KB of dynamic LDS (four groups of 64 envs: up to 144 KB) is allowed once per kernel; a
+// refusal surfaces as the launch's error
+template <int TT, bool REQ, int ENVS>
+static void launch_ref_day2_envs(dim3 grid, dim3 block, size_t lds, hipStream_t stream, const Params &p,
+                                 const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10, int i1) {
+    static const hipError_t set = hipFuncSetAttribute(reinterpret_cast<const void *>(ref_day2_kernel<TT, REQ, ENVS>),
+                                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                      (int)ref_day2_lds_bytes(REQ, ENVS));
+    (void)set;
+    hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, ENVS>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1);
+}
+
 template <int TT, bool REQ>
 static void launch_ref_day2(const Params &p, const DeviceState &s, const RefStreams &rs, int64_t E, int i4, int i10,
                             int i1, hipStream_t stream) {
     const int envs = ref_day2_envs(E);
-    const dim3 grid((unsigned)((E + envs - 1) / envs)), block(kRefBlock);
+    const int64_t per = (int64_t)envs * kRefGroups;   // envs per workgroup
+    const dim3 grid((unsigned)((E + per - 1) / per)), block(kRefBlock);
     const size_t lds = ref_day2_lds_bytes(REQ, envs);
     switch (envs) {
-        case 8: hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, 8>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
-        case 16: hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, 16>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
-        case 32: hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, 32>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
-        default: hipLaunchKernelGGL((ref_day2_kernel<TT, REQ, 64>), grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
+        case 8: launch_ref_day2_envs<TT, REQ, 8>(grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
+        case 16: launch_ref_day2_envs<TT, REQ, 16>(grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
+        case 32: launch_ref_day2_envs<TT, REQ, 32>(grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
+        default: launch_ref_day2_envs<TT, REQ, 64>(grid, block, lds, stream, p, s, rs, E, i4, i10, i1); break;
     }
 }
 

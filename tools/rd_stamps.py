@@ -49,7 +49,7 @@ def main():
         if day > 0:
             raw = buf.view(-1, 8)[:blocks].cpu().numpy()
             rows.append(raw[:, :5].astype(np.float64) * 10.0)   # ns
-            ids.append(raw[:, [7, 5]])
+            ids.append(raw[:, [6, 7, 5]])
         for t in range(24):
             venv.step_tensors(acts[t])
     venv.close()
@@ -65,15 +65,22 @@ def main():
     print("  drawing wavefront: phase 1 (draws, refills)   ", q(st[..., 2]))
     print("  timeline wavefront: phase 2 (walk, stores)    ", q(st[..., 3]))
     print("  timeline wavefront ends after the drawing one ", q(st[..., 4] - st[..., 1]))
-    # HW_ID: wave slot bits 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13 (gfx9); XCC is not in it, so the CU key
-    # here merges the same CU number of the eight XCDs
+    # HW_ID (gfx9): wave slot bits 3:0, SIMD 5:4, CU 11:8, SH 12, SE 15:13; with the XCC id a SIMD's key
     hw = ids[-1].astype(np.int64)
-    simd = (hw >> 4) & 3
-    cu = (hw >> 8) & 0xffff
-    same = np.mean((cu[:, 0] == cu[:, 1]) & (simd[:, 0] == simd[:, 1]))
-    print(f"last day: both wavefronts of a workgroup on one SIMD {same:.1%}; "
-          f"SIMDs of the drawing wavefronts {np.bincount(simd[:, 0], minlength=4).tolist()}, "
-          f"of the timeline wavefronts {np.bincount(simd[:, 1], minlength=4).tolist()}")
+    dkey = (hw[:, 0] << 16) | (hw[:, 1] & 0xff30)            # drawing wavefront: XCC, SE/SH/CU, SIMD
+    wkey = ((hw[:, 2] >> 32) << 16) | (hw[:, 2] & 0xff30)    # timeline wavefront
+    keys, counts = np.unique(dkey, return_counts=True)
+    drawers = dict(zip(keys.tolist(), counts.tolist()))
+    writers = dict(zip(*[a.tolist() for a in np.unique(wkey, return_counts=True)]))
+    own_last = own[-1]
+    print(f"last day: both wavefronts of a workgroup on one SIMD {np.mean(dkey == wkey):.1%}")
+    for nd in sorted(set(drawers.values())):
+        for nw in sorted(set(writers.values()) | {0}):
+            m = np.array([drawers[int(k)] == nd and writers.get(int(k), 0) == nw for k in dkey])
+            if m.any():
+                print(f"  drawing wavefronts on a SIMD with {nd} drawing and {nw} timeline wavefronts: "
+                      f"{m.sum():4d} workgroups, own time med {np.median(own_last[m]) / 1e3:6.2f} "
+                      f"max {own_last[m].max() / 1e3:6.2f} us")
 
 
 if __name__ == "__main__":
