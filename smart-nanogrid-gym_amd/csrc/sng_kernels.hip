@@ -2688,6 +2688,11 @@ template <int TT, bool REQ, int ENVS>
 __global__ __launch_bounds__(kRefBlock) __attribute__((amdgpu_waves_per_eu(2))) void ref_day2_kernel(Params p, DeviceState s, RefStreams rs, int64_t E,
                                                              int i4, int i10, int i1) {
     extern __shared__ __attribute__((aligned(16))) uint32_t rd_lds[];
+    // At most two wavefronts per SIMD: a VGPR count above 512 / 3 (v175 reserved here; the kernel needs ~160).
+    // With room for three, the dispatcher stacked two drawing wavefronts and a timeline one on ~96 of the
+    // 1,024 SIMDs and left others with one, and those SIMDs' workgroups set the span: 86.9 -> 77.5 us,
+    // reference reset 0.128 -> 0.119 ms obs-ready (A/B, profiles/r05_ab_refday_two_wavefronts.txt)
+    asm volatile("v_mov_b32 v175, 0" ::: "v175");
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
     const int wv = w / kRefGroups, g = w % kRefGroups;   // wv 0 draws, 1 writes group g's timeline
     const int wl = (int)threadIdx.x % kWave;

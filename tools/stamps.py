@@ -100,6 +100,14 @@ def report(ph, ids):
     print("per XCC: median start / median stamp 4 (us):",
           " ".join(f"{x}:{np.median(st[xcc == x]) / 1e3:.2f}/{np.median(ph[..., 4][xcc == x]) / 1e3:.2f}"
                    for x in range(8) if (xcc == x).any()))
+    # waves sharing a SIMD (HW_ID: SIMD bits 5:4, CU 11:8, SH 12, SE 15:13; with the XCC id), last sample
+    hw = ids[-1].astype(np.int64)
+    key = ((hw[:, 0] & 0xf) << 16) | (hw[:, 1] & 0xff30)
+    _, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
+    per = cnt[inv]
+    print("waves per SIMD (last sample): " + ", ".join(
+        f"{k}: {np.sum(per == k)} waves, median stamp 4 {np.median(ph[-1, per == k, 4]) / 1e3:.2f} us, "
+        f"max {ph[-1, per == k, 4].max() / 1e3:.2f} us" for k in sorted(set(per.tolist()))))
     # block index order vs start: dispatch order
     nb = st.shape[-1]
     for part in range(4):
