@@ -3,7 +3,9 @@
 #   tools/diag/variant.sh <name> <sed expression on sng_kernels.hip>  ->  lib/libsng_<name>.so
 #   tools/diag/variant.sh <name> -p <patch against csrc/ (-p1)>         ->  lib/libsng_<name>.so
 # e.g. tools/diag/variant.sh w4 's/wide_wpb(int) { return 1; }/wide_wpb(int) { return 4; }/'
-#      tools/diag/variant.sh ringpf -p tools/diag/patches/ring_prefetch.patch
+#      tools/diag/variant.sh refold -p tools/diag/patches/ref_day2_one_wave.patch
+# A patch under tools/diag/patches/ applies to the source of the commit that added it (later kernel changes
+# can move its context); profiles/r05_ab_*.txt name the builds each A/B compared.
 # STAMPS=1 builds the diagnostic stamps build (SNG_DIAG_STAMPS) of the variant instead.
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
