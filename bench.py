@@ -223,7 +223,11 @@ def launch_ranks(args, kw):
     cpu_baseline (handed over in a file named by SNG_BENCH_CPU_BASELINE)."""
     import subprocess
     import tempfile
-    ndev = torch.cuda.device_count()   # does not initialise the GPU on this image
+    # ADVICE r5: the visible GPUs are counted in a child process, so this one never starts the HIP runtime
+    # before its CPU baseline forks (whether torch.cuda.device_count() does is an implementation detail)
+    probe = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                           capture_output=True, text=True)
+    ndev = int(probe.stdout.strip() or 0) if probe.returncode == 0 else 0
     if args.dist_backend == "nccl" and ndev < args.gpus:
         print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible GPUs for RCCL (one rank per GPU); "
               f"{ndev} visible (--dist-backend gloo shares them)", file=sys.stderr)

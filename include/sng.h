@@ -233,6 +233,18 @@ int sng_set_seed(SngEnv *env, uint64_t seed, void *stream);
 int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done,
              const SngInfo *info, void *stream);
 
+/* sng_step with the actions in host memory and the outputs returned to host memory: the one-env gym path
+   (smart_nanogrid_environment.py:140-188 as SB3's DummyVecEnv and solvers/evaluator.py:13-24 drive it: one
+   step per call, results on the host).  actions [E][act_dim] f32, obs [E][obs_dim] f32, reward [E] f64,
+   done [E] u8 and step_flags [E] u32 (each env's SNG_FLAG_* bits raised in this step; the sticky per-env flags
+   and the flag summary are updated as by sng_step) are ordinary host memory of the caller.  The step kernel
+   reads the actions from and writes the outputs to a per-handle block of mapped host memory, so the call is
+   one kernel dispatch and one wait on `stream` (synchronous: returns when the outputs are in the caller's
+   arrays).  info as sng_step, except that SngInfo.flags must be null.  Meant for small batches; a large one
+   belongs on sng_step with device buffers. */
+int sng_step_host(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done, uint32_t *step_flags,
+                  const SngInfo *info, void *stream);
+
 /* The kernel name (as rocprofv3 reports it) of the step kernel sng_step would launch next with this
  * `info` (NULL allowed): "void sng::step_lean_kernel<N, PK, REQ>" for stations of N in {1,2,4,8,10,16}
  * chargers stepped with one lane per env, no diagnostics, NumPy-2 promotion, a power-of-two dt,

@@ -713,7 +713,7 @@ struct StepConst {
 
 // Threads per workgroup of the lean step kernel: one wavefront (1,024 workgroups at E = 65,536).
 // A/B on one box (day of 65,536 x 10): 64 threads 6.33-6.38 us per step, 256 threads 6.47-6.55,
-// 128 threads 7.13-7.14 (tools/gpu_session.sh ablib).
+// 128 threads 7.13-7.14 (library A/B: tools/diag/variant.sh builds, tools/gpu_session.sh ablib runs them).
 constexpr int kLeanBlock = 64;
 
 template <int NC>
@@ -1972,7 +1972,7 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 // (step_kernel, t = 0), so no block of this grid waits on another.
 // The timeline records leave as streaming (nontemporal) stores: reset 24.5-24.7 -> 22.5-22.7 us per day
 // at 65,536 x 10 (A/B, one box), the steps' code and state staying in L2.  Diagnostic builds
-// (tools/gpu_session.sh ablib) split the reset's time: without the t = 0 observation blocks 24.3-24.9 us
+// (round 2's -DSNG_GX_* builds, in commits before 8be1f55) split the reset's time: without the t = 0 observation blocks 24.3-24.9 us
 // (they run beside the timeline blocks), without phase 1's draws 20.7, without the record stores 16-16.8.
 // Write-through record stores (sc1 | nt, sc0 | sc1 | nt) left the day and the reset unchanged (A/B,
 // profiles/r03_ab_generator_store_policy.txt).
@@ -2151,7 +2151,7 @@ struct LaunchEvents {
 };
 
 // Stations of 10 chargers without V2X (the headline configuration) step through the wide kernel with two
-// lanes per env: A/B at 65,536 x 10 x 24 (tools/ab_headline.sh, three runs each) 6.47-6.51 us per step
+// lanes per env: A/B at 65,536 x 10 x 24 (round 3's tools/ab_headline.sh, in commits before 8be1f55; three runs each) 6.47-6.51 us per step
 // in the day graph vs 6.67-6.71 for the lean kernel, day 0.1749-0.1761 vs 0.1796-0.1803 ms; one lane per
 // env 6.75-6.79, four 8.15-8.23.  With V2X a discharging action is routine, and the lean kernel's LDS rows
 // keep numpy's order cheaper than the wide kernel's rolled re-read.
@@ -2189,7 +2189,7 @@ static bool wide_step(const Params &p, bool diag) {
 }
 
 // Lanes per env of the wide lean step kernel: two (2,048 wavefronts at 65,536 envs, two per SIMD).
-// A/B at config 5 (tools/wide_ab.sh, two runs each): 1 lane 25.85-25.91 us per step in the day graph,
+// A/B at config 5 (round 3's tools/wide_ab.sh, in commits before 8be1f55; two runs each): 1 lane 25.85-25.91 us per step in the day graph,
 // 2 lanes 22.54-22.62, 4 lanes 30.36-30.49 (128 VGPRs: 40 spilled to scratch).
 __host__ __device__ constexpr int wide_lanes(int) { return 2; }
 
@@ -2696,7 +2696,10 @@ __global__ __launch_bounds__(kRefBlock) __attribute__((amdgpu_waves_per_eu(2))) 
     // At most two wavefronts per SIMD: a VGPR count above 512 / 3 (v175 reserved here; the kernel needs ~160).
     // With room for three, the dispatcher stacked two drawing wavefronts and a timeline one on ~96 of the
     // 1,024 SIMDs and left others with one, and those SIMDs' workgroups set the span: 86.9 -> 77.5 us,
-    // reference reset 0.128 -> 0.119 ms obs-ready (A/B, profiles/r05_ab_refday_two_wavefronts.txt)
+    // reference reset 0.128 -> 0.119 ms obs-ready (A/B, profiles/r05_ab_refday_two_wavefronts.txt).  This assumes
+    // gfx950's 512 VGPRs per SIMD lane with an allocation granule of 8 (176 > 512 / 3); tests/test_kernel_resources.py
+    // reads the built code object's VGPR count and fails when the cap no longer holds
+    // (profiles/r06_kernel_resources.txt: without this line the compiler allocates 158 VGPRs, three per SIMD).
     asm volatile("v_mov_b32 v175, 0" ::: "v175");
     const int w = __builtin_amdgcn_readfirstlane((int)threadIdx.x / kWave);
     const int wv = w / kRefGroups, g = w % kRefGroups;   // wv 0 draws, 1 writes group g's timeline

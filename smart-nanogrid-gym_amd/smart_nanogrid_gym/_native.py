@@ -116,6 +116,8 @@ EXPORTS = {
     "sng_reset_from_scenario": (ctypes.c_int, [_H, ctypes.POINTER(SngScenario), ctypes.c_void_p, _S]),
     "sng_step": (ctypes.c_int, [_H, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.c_void_p, ctypes.POINTER(SngInfo), _S]),
+    "sng_step_host": (ctypes.c_int, [_H, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.POINTER(SngInfo), _S]),
     "sng_step_kernel_name": (ctypes.c_int, [_H, ctypes.POINTER(SngInfo), ctypes.c_char_p, ctypes.c_int32]),
     "sng_read_errors": (ctypes.c_int, [_H, c_uint32_p, ctypes.c_int, _S]),
     "sng_get_battery_soc": (ctypes.c_int, [_H, c_double_p, _S]),

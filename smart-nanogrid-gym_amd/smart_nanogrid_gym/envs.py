@@ -5,11 +5,14 @@ implementation with num_envs = 1.
 Same constructor keywords, same spaces, reset() -> (obs, {}), step(a) ->
 (obs float32[obs_dim], reward float64, terminated, False, {}).
 """
+import ctypes
+
 import numpy as np
 import torch
 
+from ._native import check, lib
 from .recorder import DayRecorder
-from .vec_env import SmartNanogridVecEnv
+from .vec_env import SmartNanogridVecEnv, _stream_handle
 
 try:  # subclass gym(nasium).Env when available so wrappers / checkers accept it
     import gymnasium as _gym   # pragma: no cover - not in the image
@@ -49,6 +52,14 @@ class SmartNanogridEnv(_Base):
         self.simulated_single_day = False
         self.timestep = None
         self.recorder = DayRecorder(self._venv, [0], results_directory) if results_directory is not None else None
+        # step(): "host" = one sng_step_host call (the step kernel reads the actions from and writes its outputs
+        # to mapped host memory: one dispatch and one wait); "torch" = the VecEnv's device buffers with torch
+        # copies (round 5's path; a recorder or per-step diagnostics need it, as they read device arrays)
+        self.step_path = "host"
+        self._rew1 = np.zeros(1, np.float64)
+        self._done1 = np.zeros(1, np.uint8)
+        self._flags1 = np.zeros(1, np.uint32)
+        self._out_ptrs = [ctypes.c_void_p(x.ctypes.data) for x in (self._rew1, self._done1, self._flags1)]
 
     def reset(self, generate_new_initial_values=True, algorithm_used="", environment_mode="", **kwargs):
         """smart_nanogrid_environment.py:311-351 (gym-0.26 `seed=`/`options=` are accepted and ignored,
@@ -67,6 +78,19 @@ class SmartNanogridEnv(_Base):
         if self.simulated_single_day:
             raise RuntimeError("the simulated day is over: call reset()")
         v = self._venv
+        if self.step_path == "host" and not v._recorders and not v.info_d:
+            a = np.ascontiguousarray(actions, dtype=np.float32)
+            if a.size != v.act_dim:
+                raise ValueError(f"actions must have {v.act_dim} elements")
+            obs = np.empty(v.obs_dim, np.float32)
+            check(lib().sng_step_host(v._h, a.ctypes.data, obs.ctypes.data, *self._out_ptrs, ctypes.byref(v._info),
+                                      _stream_handle(v.device)), v._h)
+            if self._flags1[0]:
+                v._raise_flags(v._read_and_clear_flags())
+            terminated = bool(self._done1[0])
+            self.timestep = 0 if terminated else self.timestep + 1
+            self.simulated_single_day = terminated
+            return obs, np.float64(self._rew1[0]), terminated, False, {}
         v._act_h.numpy()[0] = np.asarray(actions, dtype=np.float32).reshape(-1)
         with torch.cuda.device(v.device):
             v.actions_d.copy_(v._act_h, non_blocking=True)

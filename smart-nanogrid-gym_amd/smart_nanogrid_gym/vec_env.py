@@ -20,8 +20,10 @@ Reference behaviour mirrored per env (smart_nanogrid_gym/envs/smart_nanogrid_env
   step(a)  -> (obs float32, reward = -total cost float64, terminated, truncated=False, {}) (:140-188)
   errors   -> the reference's ValueErrors, raised after the step that hit them
 """
+import collections.abc
 import ctypes
 import itertools
+import operator
 import time
 import warnings
 
@@ -49,6 +51,104 @@ def _empty_infos(n):
     """n distinct empty dicts (SB3's per-env infos): dict() mapped over a repeat runs in C, about a quarter
     faster than a list comprehension of {} at 65,536 envs."""
     return list(itertools.starmap(dict, itertools.repeat((), n)))
+
+
+class StepInfos(collections.abc.Sequence):
+    """SB3's per-env `infos` of one step, list-compatible and made on access.
+
+    DummyVecEnv returns a list of num_envs fresh dicts: {} for a running env, and for an env whose day just
+    ended {"terminal_observation": its last observation, "TimeLimit.truncated": False} (solvers/RL/ppo_train.py
+    hands the env to SB3, whose rollout reads infos[i] of done envs).  At 65,536 envs building those dicts cost
+    ~0.5 ms every step and, once a day, ~5.5 ms for the terminal ones (a numpy row view each;
+    profiles/r05_sb3_path.log).  Here an env's dict is built the first time it is indexed (`infos[i]`, then
+    cached, so writes through it persist, as VecNormalize's `infos[i]["terminal_observation"] = ...` needs);
+    iterating, slicing, `list(infos)`, `infos.copy()` and comparison build the dicts they cover in bulk.
+    Whatever is built holds exactly what DummyVecEnv's dict would, including the `v2x_breakpoint` entries of
+    the reference's V2X breakpoint (central_management_system.py:160-165).  Pickling and deep copies give a
+    plain list."""
+
+    __slots__ = ("_n", "_terminal", "_done", "_v2x", "_made", "_all")
+
+    def __init__(self, n, terminal_obs=None, done=None, v2x=()):
+        self._n = int(n)
+        self._terminal = terminal_obs        # [n, obs_dim] array holding the done envs' last observations
+        self._done = done                    # bool [n]: the envs whose dict carries terminal_observation
+        self._v2x = frozenset(int(i) for i in v2x)
+        self._made = {}                      # index -> the dict handed out
+        self._all = None                     # the whole list, once built
+
+    def __len__(self):
+        return self._n
+
+    def _make(self, i):
+        d = self._made.get(i)
+        if d is None:
+            d = {}
+            if self._terminal is not None and self._done[i]:
+                d["terminal_observation"] = self._terminal[i]
+                d["TimeLimit.truncated"] = False
+            if i in self._v2x:
+                d["v2x_breakpoint"] = True
+            self._made[i] = d
+        return d
+
+    def _build_all(self):
+        """Every env's dict, as one list (the dicts already handed out keep their identity)."""
+        if self._all is None:
+            n = self._n
+            if self._terminal is not None and self._done.all():
+                out = [{"terminal_observation": o, "TimeLimit.truncated": False} for o in self._terminal]
+            elif self._terminal is not None:
+                out = _empty_infos(n)
+                for i in np.nonzero(self._done)[0].tolist():
+                    out[i].update(terminal_observation=self._terminal[i], **{"TimeLimit.truncated": False})
+            else:
+                out = _empty_infos(n)   # dict() over a repeat, in C (~8 ns a dict)
+            for i in self._v2x:
+                out[i]["v2x_breakpoint"] = True
+            for i, d in self._made.items():
+                out[i] = d
+            self._all = out
+            self._made = dict(enumerate(out))
+        return self._all
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            if self._all is not None:
+                return self._all[i]
+            r = range(*i.indices(self._n))
+            return self._build_all()[i] if len(r) > 64 else [self._make(k) for k in r]
+        i = operator.index(i)
+        if i < 0:
+            i += self._n
+        if not 0 <= i < self._n:
+            raise IndexError("infos index out of range")
+        return self._make(i) if self._all is None else self._all[i]
+
+    def __iter__(self):
+        return iter(self._build_all())
+
+    def __reversed__(self):
+        return reversed(self._build_all())
+
+    def copy(self):
+        return list(self._build_all())
+
+    def __eq__(self, other):
+        if isinstance(other, StepInfos):
+            other = other._build_all()
+        return isinstance(other, list) and self._build_all() == other
+
+    __hash__ = None
+
+    def __add__(self, other):
+        return self._build_all() + list(other)
+
+    def __reduce__(self):
+        return (list, (self._build_all(),))
+
+    def __repr__(self):
+        return f"StepInfos({self._build_all()!r})"
 
 
 def _host_copy(pinned):
@@ -363,12 +463,12 @@ class SmartNanogridVecEnv(_VecEnvBase):
 
     def step_wait(self):
         """The numpy step SB3 drives (DummyVecEnv semantics).  Device work: the actions' H2D copy, the step and
-        one D2H copy of its outputs (reward, observation, done, flag summary).  Host work while the device
-        runs: the per-env info dicts.  A done step (the day's last) raises the day's flags, then enqueues the
-        automatic reset (the next day and its observation's D2H copy) before it builds the 65,536
-        terminal_observation infos, so the reset runs on the device under that host work.  Host copies of the
-        observations go through torch's multi-threaded CPU copy (a fresh array per step, as DummyVecEnv
-        returns copies)."""
+        one D2H copy of its outputs (reward, observation, done, flag summary).  A done step (the day's last)
+        raises the day's flags, then enqueues the automatic reset (the next day and its observation's D2H
+        copy), and the host copies the terminal observations while the device resets.  The infos are a
+        StepInfos: each env's dict (terminal_observation on a done step) is made when it is first accessed.
+        Host copies of the observations go through torch's multi-threaded CPU copy (a fresh array per step,
+        as DummyVecEnv returns copies)."""
         actions = self._pending
         self._pending = None
         E = self.num_envs
@@ -379,7 +479,6 @@ class SmartNanogridVecEnv(_VecEnvBase):
         if prof is not None:
             ta = time.perf_counter()
         stream = torch.cuda.current_stream(self.device)
-        last = lib().sng_get_timestep(self._h) + 1 >= self.timesteps
         with torch.cuda.device(self.device):
             if prof is not None:
                 ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
@@ -394,8 +493,6 @@ class SmartNanogridVecEnv(_VecEnvBase):
             if prof is not None:
                 ev[3].record(stream)
                 t1 = time.perf_counter()
-            # the per-env info dicts SB3 expects (one fresh dict per env) are built while the device works
-            infos = None if last else _empty_infos(E)
             stream.synchronize()
         if prof is not None:
             t2 = time.perf_counter()
@@ -405,6 +502,7 @@ class SmartNanogridVecEnv(_VecEnvBase):
         obs = _host_copy(self._obs_h)
         rewards = _host_copy(self._rew_h)
         dones = self._done_h.numpy().astype(bool)
+        v2x = () if flags is None else np.nonzero(flags & _native.FLAG_V2X_BREAKPOINT)[0].tolist()
         if prof is not None:
             t3 = time.perf_counter()
         if dones.any():
@@ -419,10 +517,9 @@ class SmartNanogridVecEnv(_VecEnvBase):
                 if prof is not None:
                     ev[5].record(stream)
                     t4 = time.perf_counter()
-                infos = [{"terminal_observation": o, "TimeLimit.truncated": False} for o in obs]
-                if flags is not None:
-                    for i in np.nonzero(flags & _native.FLAG_V2X_BREAKPOINT)[0]:
-                        infos[i]["v2x_breakpoint"] = True
+                # the terminal observations stay in `obs` (this step's fresh copy); each env's
+                # terminal_observation is a row of it, made when its info is accessed
+                infos = StepInfos(E, obs, dones, v2x)
                 if prof is not None:
                     t5 = time.perf_counter()
                 stream.synchronize()
@@ -437,9 +534,7 @@ class SmartNanogridVecEnv(_VecEnvBase):
                     prof.setdefault(k, []).append(x)
                 prof.setdefault("reset_device", []).append(ev[4].elapsed_time(ev[5]) * 1e-3)
         else:
-            if flags is not None:
-                for i in np.nonzero(flags & _native.FLAG_V2X_BREAKPOINT)[0]:
-                    infos[i]["v2x_breakpoint"] = True
+            infos = StepInfos(E, v2x=v2x)
         if prof is not None:
             for k, x in (("actions_in", ta - t0), ("enqueue", t1 - ta), ("sync", t2 - t1), ("host_out", t3 - t2)):
                 prof.setdefault(k, []).append(x)

@@ -108,3 +108,61 @@ def load_vec_env_with_sb3():
             else:
                 sys.modules[k] = v
     return module
+
+
+# The ways SB3 2.x's own code reads a VecEnv's `infos` (restated from its published sources, SB3 is not
+# installed): each takes (obs, rewards, dones, infos) as step_wait returns them and gives what SB3 keeps.
+def vec_monitor_step(rewards, dones, infos, returns, lengths):
+    """VecMonitor.step_wait: `new_infos = list(infos[:])`, a copied dict with an "episode" entry for each done
+    env, the running returns and lengths reset there."""
+    returns += rewards
+    lengths += 1
+    new_infos = list(infos[:])
+    for i in range(len(dones)):
+        if dones[i]:
+            info = infos[i].copy()
+            info["episode"] = {"r": float(returns[i]), "l": int(lengths[i]), "t": 0.0}
+            returns[i] = 0.0
+            lengths[i] = 0
+            new_infos[i] = info
+    return new_infos
+
+
+def update_info_buffer(infos, dones, ep_info_buffer):
+    """BaseAlgorithm._update_info_buffer: every env's info is read with .get()."""
+    for idx, info in enumerate(infos):
+        maybe_ep_info = info.get("episode")
+        if maybe_ep_info is not None:
+            ep_info_buffer.append(maybe_ep_info)
+        assert info.get("is_success") is None
+
+
+def timeout_bootstrap_envs(dones, infos):
+    """OnPolicyAlgorithm.collect_rollouts: the done envs whose day was truncated (their terminal_observation is
+    bootstrapped through the value net)."""
+    return [idx for idx, done in enumerate(dones)
+            if done and infos[idx].get("terminal_observation") is not None
+            and infos[idx].get("TimeLimit.truncated", False)]
+
+
+def store_transition_next_obs(new_obs, dones, infos):
+    """OffPolicyAlgorithm._store_transition: the next observation of a done env is its terminal_observation."""
+    next_obs = new_obs.copy()
+    for i, done in enumerate(dones):
+        if done and infos[i].get("terminal_observation") is not None:
+            next_obs[i] = infos[i]["terminal_observation"]
+    return next_obs
+
+
+def replay_buffer_timeouts(infos):
+    """ReplayBuffer.add(handle_timeout_termination=True)."""
+    return np.array([info.get("TimeLimit.truncated", False) for info in infos])
+
+
+def vec_normalize_terminal(dones, infos, scale):
+    """VecNormalize.step_wait: the done envs' terminal_observation is replaced in place."""
+    for idx, done in enumerate(dones):
+        if not done:
+            continue
+        if "terminal_observation" in infos[idx]:
+            infos[idx]["terminal_observation"] = infos[idx]["terminal_observation"] * scale

@@ -7,6 +7,7 @@ numbers (libm pow(x, 2), which is off by one ulp on ~0.1 % of inputs) within 1e-
 relative -- far inside the 1e-5 the north star allows.
 """
 import ctypes
+import warnings
 
 import numpy as np
 import pytest
@@ -363,6 +364,60 @@ def test_single_env_gym_surface():
         assert isinstance(r, np.float64) and trunc is False and term == (t == 23)
     with pytest.raises(RuntimeError):
         env.step(d["actions"][0][0])
+    env.close()
+
+
+@pytest.mark.parametrize("n,v2x,rng", [(10, False, "reference"), (4, False, "device"), (10, True, "reference"),
+                                       (7, False, "reference")])
+def test_single_env_host_step_equals_device_buffer_step(n, v2x, rng):
+    """SmartNanogridEnv.step's sng_step_host path (the kernel reads the actions from and
+    writes its outputs to mapped host memory) gives bit for bit what round 5's torch path gives (device
+    buffers, copies), over three days of each station kernel: the wide kernel (N = 10), the lean one (N = 4,
+    V2X at N = 10) and the general one (N = 7); V2X days raise the reference's breakpoint warning through the
+    host path's flags."""
+    kw = dict(number_of_chargers=n, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="sparse", vehicle_to_everything=v2x)
+    envs = [SmartNanogridEnv(seed=31, rng=rng, **kw) for _ in range(2)]
+    envs[1].step_path = "torch"
+    rng_a = np.random.default_rng(n)
+    lo, hi = envs[0].action_space.low, envs[0].action_space.high
+    warned = []
+    for day in range(3):
+        o0, o1 = envs[0].reset()[0], envs[1].reset()[0]
+        np.testing.assert_array_equal(o0, o1)
+        for t in range(24):
+            a = (lo + (hi - lo) * rng_a.random(lo.size)).astype(np.float32)
+            a[rng_a.random(a.size) < 0.2] = 0
+            with warnings.catch_warnings(record=True) as w:
+                warnings.simplefilter("always")
+                r0 = envs[0].step(a)
+                r1 = envs[1].step(a)
+            warned += [str(x.message) for x in w]
+            np.testing.assert_array_equal(r0[0], r1[0])
+            assert r0[0].dtype == np.float32 and r0[0].shape == envs[0].observation_space.shape
+            assert isinstance(r0[1], np.float64) and r0[1] == r1[1] and r0[2:] == r1[2:] and r0[2] == (t == 23)
+    assert envs[0].timestep == 0 and envs[0].simulated_single_day
+    if v2x:
+        assert any("breakpoint" in m for m in warned)
+    for e in envs:
+        e.close()
+
+
+def test_single_env_host_step_raises_reference_errors():
+    """The host path's per-step flags raise the reference's ValueError at the step that hit it (charging_mode=''
+    leaves the positive-action branch unimplemented, charger.py:88) and refuse a wrong action size."""
+    env = SmartNanogridEnv(number_of_chargers=3, time_interval="1h", charging_mode="",
+                           vehicle_uncharged_penalty_mode="sparse", seed=3)
+    env.reset()
+    with pytest.raises(ValueError, match="charging mode"):
+        for _ in range(24):
+            env.step(np.ones(4, np.float32))
+    env.close()
+    env = SmartNanogridEnv(number_of_chargers=3, time_interval="1h", charging_mode="bounded",
+                           vehicle_uncharged_penalty_mode="sparse", seed=3)
+    env.reset()
+    with pytest.raises(ValueError, match="4 elements"):
+        env.step(np.ones(5, np.float32))
     env.close()
 
 

@@ -55,6 +55,12 @@ for s in $STEPS; do
     sb3ab) for i in 1 2; do SNG_LIBRARY=smart-nanogrid-gym_amd/lib/libsng.so run "sb3_old$i" 300 python tools/sb3_path_bench.py --pkg tools/diag/old_pkg
                             run "sb3_new$i" 300 python tools/sb3_path_bench.py; done
            run host_copy 120 python tools/host_copy_bench.py ;;
+    single) run single_env_host 300 python tools/single_env_bench.py
+            run single_env_torch 300 python tools/single_env_bench.py --path torch
+            SNG_STEP_HOST_COPY=1 run single_env_hostcopy 300 python tools/single_env_bench.py
+            run single_env_device 300 python tools/single_env_bench.py --rng device ;;
+    iolat) run io_latency 120 tools/io_latency ;;
+    sb3c)  run sb3_consume 600 python tools/sb3_path_bench.py --consume ;;
     sb3)   run sb3_path 600 python tools/sb3_path_bench.py
            run sb3_path_device 600 python tools/sb3_path_bench.py --rng device ;;
     pmc5)  run pmc5_fetch 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/pmc5_fetch -o run --output-format csv -- python bench.py --no-cpu-baseline --chargers 50 --time-interval 15min --extended-day --pv-noise 0.2 --price-noise 0.1 --steps 2 --warmup 1 --graph-days 1 --timing-days 1

@@ -3,7 +3,7 @@ dones, infos) with numpy actions in and numpy results out, automatic reset at th
 default reference RNG (solvers/RL/ppo_train.py:89-102 hands the env to PPO, whose collect_rollouts calls
 env.step(clipped_actions) once per rollout step).
 
-    python tools/sb3_path_bench.py [--envs 65536] [--days 20] [--rng reference|device]
+    python tools/sb3_path_bench.py [--envs 65536] [--days 20] [--rng reference|device] [--consume]
 
 Prints one JSON line: env-steps/s over whole days (the 24 steps of each day, its automatic reset included),
 and the split of one step into its phases, each the median over the timed steps:
@@ -41,6 +41,10 @@ def main():
     ap.add_argument("--warmup-days", type=int, default=1)
     ap.add_argument("--rng", default="reference", choices=["reference", "device"])
     ap.add_argument("--pkg", default=None, help="A/B: the directory holding another smart_nanogrid_gym package")
+    ap.add_argument("--consume", action="store_true",
+                    help="after every step, read the infos as SB3 2.x's PPO rollout does (its info buffer update "
+                         "over every env's info and the timeout-bootstrap check; tests/sb3_stub.py restates both) "
+                         "and time that as `consumer_ms_per_step`")
     args = ap.parse_args()
     if args.pkg:
         sys.path.insert(0, os.path.abspath(args.pkg))
@@ -61,12 +65,22 @@ def main():
     venv.reset()
     for i in range(args.warmup_days * T):
         venv.step(pool[i % len(pool)])
+    if args.consume:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import sb3_stub as S
+    consumer = []
+    ep_buf = []
     venv.profile_phases(True)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     n = args.days * T
     for i in range(n):
         obs, rew, done, infos = venv.step(pool[i % len(pool)])
+        if args.consume:
+            tc = time.perf_counter()
+            S.update_info_buffer(infos, done, ep_buf)
+            S.timeout_bootstrap_envs(done, infos)
+            consumer.append(time.perf_counter() - tc)
     elapsed = time.perf_counter() - t0
     ph = venv.profile_phases(False)
     assert obs.shape == (E, venv.obs_dim) and np.isfinite(rew).all() and len(infos) == E
@@ -76,7 +90,9 @@ def main():
            "timesteps": T, "days": args.days, "rng": args.rng, "ms_per_step": elapsed / n * 1e3,
            "split_ms_median": split,
            "note": "reset* are per day (one automatic reset per 24 steps); every other phase per step",
-           "reset_ms_per_day_mean": round(float(np.mean(ph["reset"])) * 1e3, 4) if ph.get("reset") else None}
+           "reset_ms_per_day_mean": round(float(np.mean(ph["reset"])) * 1e3, 4) if ph.get("reset") else None,
+           "consumer_ms_per_step": round(float(np.mean(consumer)) * 1e3, 4) if consumer else None,
+           "value_without_consumer": (E * n / (elapsed - sum(consumer))) if consumer else None}
     print(json.dumps(out))
     venv.close()
 
