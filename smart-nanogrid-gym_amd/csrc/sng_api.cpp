@@ -516,11 +516,11 @@ struct SngEnv {
     RefStreams ps{};                  // Python's `random` stream of every env, on the device (py_ratio_lane in observe0_kernel)
     bool py_seeded = false;
     // sng_step_host's I/O block: the step kernel reads its actions from and writes its outputs to host memory
-    // (mapped, coherent), so a host-driven step is one dispatch and one wait (zero-copy); hio_copy: the
-    // staged alternative (device block + two copies), kept for the A/B of tools/single_env_bench.py
-    char *hio = nullptr, *hio_dev = nullptr, *hio_stage = nullptr;
+    // (mapped, coherent), so a host-driven step is one dispatch and one wait.  A/B (profiles/r06_single_env.log,
+    // SmartNanogridEnv.step at N = 10): 21.7 us per call against 25.4 us staged through a device block with a
+    // copy each way, and 34.2 us for round 5's torch copies; tools/io_latency.hip: 13.0 / 17.2 us in C
+    char *hio = nullptr, *hio_dev = nullptr;
     size_t hio_bytes = 0;
-    int hio_copy = -1;
     std::string err;
 
     size_t timeline() const { return (size_t)p.T * p.n * (size_t)E; }
@@ -1064,7 +1064,6 @@ void sng_destroy(SngEnv *env) {
         if (x) (void)hipHostFree(x);
     if (env->staging_done) (void)hipEventDestroy(env->staging_done);
     if (env->hio) (void)hipHostFree(env->hio);
-    if (env->hio_stage) (void)hipFree(env->hio_stage);
     delete env;
 }
 
@@ -1309,29 +1308,21 @@ int sng_step_host(SngEnv *env, const float *actions, float *obs, double *reward,
     // [actions E x A f32 | obs E x O f32 | reward E f64 | done E u8 | flags E u32], sections 256 B aligned
     const size_t o_obs = al(E * A * 4), o_rew = o_obs + al(E * O * 4), o_done = o_rew + al(E * 8),
                  o_fl = o_done + al(E), bytes = o_fl + al(E * 4);
-    if (env->hio_copy < 0) {
-        const char *v = std::getenv("SNG_STEP_HOST_COPY");
-        env->hio_copy = (v && v[0] == '1') ? 1 : 0;
-    }
     if (env->hio_bytes < bytes) {
         if (env->hio) (void)hipHostFree(env->hio);
-        if (env->hio_stage) (void)hipFree(env->hio_stage);
-        env->hio = env->hio_dev = env->hio_stage = nullptr;
+        env->hio = env->hio_dev = nullptr;
         env->hio_bytes = 0;
         HIP_TRY(env, hipHostMalloc((void **)&env->hio, bytes, hipHostMallocMapped | hipHostMallocCoherent));
         HIP_TRY(env, hipHostGetDevicePointer((void **)&env->hio_dev, env->hio, 0));
-        if (env->hio_copy) HIP_TRY(env, hipMalloc((void **)&env->hio_stage, bytes));
         env->hio_bytes = bytes;
     }
-    char *h = env->hio, *d = env->hio_copy ? env->hio_stage : env->hio_dev;
+    char *h = env->hio, *d = env->hio_dev;
     std::memcpy(h, actions, E * A * 4);
-    if (env->hio_copy) HIP_TRY(env, hipMemcpyAsync(d, h, E * A * 4, hipMemcpyHostToDevice, st));
     InfoPtrs ip = info_ptrs(info);
     ip.flags = reinterpret_cast<uint32_t *>(d + o_fl);   // this step's flags of every env (the sticky ones stay)
     HIP_TRY(env, launch_step(env->p, env->ds, ip, env->host_tab, reinterpret_cast<const float *>(d),
                              reinterpret_cast<float *>(d + o_obs), reinterpret_cast<double *>(d + o_rew),
                              reinterpret_cast<uint8_t *>(d + o_done), env->E, env->t, 1, st));
-    if (env->hio_copy) HIP_TRY(env, hipMemcpyAsync(h + o_obs, d + o_obs, bytes - o_obs, hipMemcpyDeviceToHost, st));
     env->t += 1;
     if (env->t == env->p.T) env->day_finished = true;
     HIP_TRY(env, hipStreamSynchronize(st));

@@ -57,9 +57,11 @@ for s in $STEPS; do
            run host_copy 120 python tools/host_copy_bench.py ;;
     single) run single_env_host 300 python tools/single_env_bench.py
             run single_env_torch 300 python tools/single_env_bench.py --path torch
-            SNG_STEP_HOST_COPY=1 run single_env_hostcopy 300 python tools/single_env_bench.py
             run single_env_device 300 python tools/single_env_bench.py --rng device ;;
     iolat) run io_latency 120 tools/io_latency ;;
+    genab) for l in ${AB_LIBS:?}; do SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "genab_$l" 300 python tools/diag/gen_ab_check.py; done
+           set -- ${AB_LIBS}; if diff <(grep '^E=' $OUT/genab_$1.log) <(grep '^E=' $OUT/genab_$2.log) > $OUT/genab_diff.txt; then echo "genab: identical" | tee -a $OUT/session.log; else echo "genab: DIFFER" | tee -a $OUT/session.log; fi ;;
+    sqsalu) for l in ${SQ_LIBS:-libsng}; do SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "sqsalu_$l" 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU -d $OUT/sqsalu_$l -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1; done ;;
     sb3c)  run sb3_consume 600 python tools/sb3_path_bench.py --consume ;;
     sb3)   run sb3_path 600 python tools/sb3_path_bench.py
            run sb3_path_device 600 python tools/sb3_path_bench.py --rng device ;;
