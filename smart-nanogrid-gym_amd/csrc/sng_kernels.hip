@@ -1991,96 +1991,6 @@ constexpr uint32_t kVehRecMask = 0x3fff8u;         // capacity (3-9) and departu
 // holds (rec_carry), computed once per vehicle in phase 1.  TT: the day's step count as
 // a compile-time constant (the walk unrolled: 24 for the 1 h day), 0 for a runtime p.T; REQ: the
 // requested-SoC stream.
-// Bits [a, b] of a 64-bit mask (0 when a > b); a >= 0, b <= 63.
-__device__ __forceinline__ uint64_t bit_range64(int a, int b) {
-    return a > b ? 0ull : (2ull << b) - (1ull << a);
-}
-constexpr uint64_t kOddBits = 0xaaaaaaaaaaaaaaaaull;
-
-// The timeline of one (env, charger) of a day of at most 32 steps (the 1 h day), as bit masks over the steps
-// (round 6).  Phase 1 draws the day's vehicles exactly as the list walk below does (the same draws of the same
-// counter-based stream: vehicle v takes draws 2v and 2v + 1), but unrolled over the VMAX vehicles a day can
-// hold and branch-free (a vehicle arriving at or after T is not kept; every later one arrives later still), and
-// sets per vehicle: its steps in `occm`, its arrival step in `spm` bit 2t (STATIC), the steps its stay puts in
-// observe(t-1)'s penalty-check list in `spm` bit 2t + 1 (PEN), and its departure step in `advm`.  Phase 2 then
-// writes step t's record from the masks and the entry of the vehicle that "owns" the step -- the one present,
-// or on an empty step the next to arrive, whose SoC code an empty record before an arrival carries -- the owner
-// advancing at each departure step.  Per step: ~15 VALU, one LDS read (the owner after the next, a step
-// ahead), one store, and no scalar work: the list walk's per-step lane-mask logic and per-plane buffer
-// descriptors were ~10 SALU per step (247 per wavefront in phase 2), and the SALU, which a CU's four SIMDs
-// share, is what the generator's wavefronts queued on (SQ: 47.6 % of wave time ready but not issued at ~16 %
-// VALU busy, profiles/r05_sq_step_kernels.txt).  WIDE32: the whole record timeline lies within 4 GiB of its
-// base, so a plane is a 32-bit lane offset (else one buffer descriptor per plane).
-template <int TT, bool WIDE32>
-__device__ __forceinline__ void gen_walk_masks(const Params &p, const DeviceState &s, GenStream &rng, int64_t E,
-                                               int i4, int i10, int i1, int tid, int64_t e, int c, int q4, int qw,
-                                               uint32_t *s_veh, uint32_t *s_car) {
-    static_assert(TT > 0 && TT <= 32 && TT % 6 == 0, "a day of at most 32 steps, 4 / dt = TT / 6");
-    constexpr int VMAX = TT / (TT / 6 + 1) + 1;   // a vehicle stays >= 4/dt steps and leaves one step empty
-    // the penalty-check list observe(t-1) builds (charging_station.py:42-63), as the steps s = t + 1 whose
-    // vehicle at t had dep - t in [lo, lo + span] steps left: on_departure {1}, sparse {1..3}, dense any;
-    // no_penalty never (lo = 256)
-    const int plo = (p.penalty_mode == SNG_PENALTY_NONE) ? 256 : 1;
-    const int pspan = (p.penalty_mode == SNG_PENALTY_SPARSE) ? 2 : (p.penalty_mode == SNG_PENALTY_DENSE) ? 254 : 0;
-    uint32_t occm = 0u, advm = 0u;
-    uint64_t spm = 0ull;
-    int tfree = 0;
-#pragma unroll
-    for (int v = 0; v < VMAX; ++v) {
-        const VehicleDraw d = draw_vehicle(p, rng, tfree, i4, i10, i1);
-        const bool ok = d.ta < TT;
-        const int ta = ok ? d.ta : 0, dep = ok ? d.dep : 0;
-        s_veh[v * kGenBlock + tid] = ok ? ((uint32_t)d.ta << kVehArrShift) | (d.cap << P_CAP_SHIFT) |
-                                              ((uint32_t)d.dep << P_DEP_SHIFT)
-                                        : (0xffu << kVehArrShift) | (0xffu << P_DEP_SHIFT);
-        s_car[v * kGenBlock + tid] = ok ? rec_carry(false, d.code) : 0u;
-        const int dend = dep < TT ? dep : TT;
-        const int ps = (ta + 1 > dep - plo - pspan + 1) ? ta + 1 : dep - plo - pspan + 1;
-        const int pe = (dep - plo + 1 < TT - 1) ? dep - plo + 1 : TT - 1;
-        const uint64_t m = ((1ull << (2 * ta)) | (bit_range64(2 * ps + 1, 2 * pe + 1) & kOddBits));
-        const uint32_t o = (uint32_t)bit_range64(ta, dend - 1);
-        occm |= ok ? o : 0u;
-        spm |= ok ? m : 0ull;
-        advm |= (ok && dep < TT) ? 1u << (dep & 31) : 0u;
-        tfree = d.dep + 1;   // the departure step stays empty (charging_station.py:239-251)
-    }
-    s_veh[VMAX * kGenBlock + tid] = (0xffu << kVehArrShift) | (0xffu << P_DEP_SHIFT);   // a sentinel
-    s_car[VMAX * kGenBlock + tid] = 0u;
-
-    uint32_t ent = s_veh[tid], car = s_car[tid];                              // the owner of step t
-    uint32_t nent = s_veh[kGenBlock + tid], ncar = s_car[kGenBlock + tid];   // the vehicle after it
-    int nx = kGenBlock + tid;
-    uint16_t *rec = reinterpret_cast<uint16_t *>(s.aux);
-    const uint32_t nE2 = (uint32_t)((size_t)p.n * (size_t)E * 2u);   // bytes per record plane
-    const uint32_t el2 = ((uint32_t)e * (uint32_t)qw + (uint32_t)(c - q4)) * 2u + (uint32_t)q4 * (uint32_t)E * 2u;
-    uint32_t off = el2;
-    // plane 0: the SoC code of a vehicle arriving at t = 0
-    bst16<kGenRecPol>(rec, off, (spm & 1ull) ? car : 0u);
-#pragma unroll
-    for (int t = 0; t < TT; ++t) {
-        // (each condition feeds selects only, so it stays one VALU compare into VCC: no lane-mask logic)
-        const bool adv = (advm >> t) & 1u;   // a departure step: the next vehicle owns it
-        ent = adv ? nent : ent;
-        car = adv ? ncar : car;
-        nx += adv ? kGenBlock : 0;
-        nent = s_veh[nx];
-        ncar = s_car[nx];
-        const uint32_t sp = (uint32_t)(spm >> (2 * t));   // bits: STATIC at t, PEN at t, STATIC at t + 1
-        const uint32_t fl = ((sp << 1) & 6u) | W_OCC;
-        // occupied: capacity and departure in place, the departure becoming the steps left (dep > t)
-        const uint32_t w_occ = ((ent - ((uint32_t)t << P_DEP_SHIFT)) & kVehRecMask) | fl;
-        // empty: the penalty flag, and the SoC code of the vehicle arriving at t + 1
-        const uint32_t w_emp = (fl & W_PEN) | ((sp & 4u) ? car : 0u);
-        const uint32_t r = ((occm >> t) & 1u) ? w_occ : w_emp;
-        if constexpr (WIDE32) {
-            off += nE2;
-            bst16<kGenRecPol>(rec, off, r);
-        } else {
-            bst16<kGenRecPol>(rec + (size_t)(t + 1) * ((size_t)p.n * (size_t)E), el2, r);
-        }
-    }
-}
-
 template <int TT, bool REQ>
 __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceState s, uint64_t seed, int64_t E,
                                                              int i4, int i10, int i1, float *__restrict__ obs,
@@ -2114,13 +2024,6 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     GenStream rng{gen_key(seed, ge, (uint32_t)c, day), 0u};
     const int T = TT > 0 ? TT : p.T;
     const int n = p.n;
-    if constexpr (TT > 0 && TT <= 32 && !REQ) {
-        if ((uint64_t)(TT + 1) * (uint64_t)n * (uint64_t)E * 2u < (1ull << 32))
-            gen_walk_masks<TT, true>(p, s, rng, E, i4, i10, i1, tid, e, c, q4, qw, s_veh, s_car);
-        else
-            gen_walk_masks<TT, false>(p, s, rng, E, i4, i10, i1, tid, e, c, q4, qw, s_veh, s_car);
-        return;
-    }
 
     // phase 1 (charging_station.py:200-279)
     int tfree = 0, nv = 0;
@@ -2465,7 +2368,6 @@ hipError_t launch_profiles(const Params &p, const DeviceState &s, int64_t E, hip
 hipError_t launch_generate(const Params &p, const DeviceState &s, uint64_t seed, int64_t E, int i4, int i10, int i1,
                            float *obs, double *ep_return, int vec_io, hipStream_t stream, hipEvent_t ev_start,
                            hipEvent_t ev_stop) {
-    if (p.T == 24 && i4 != 4) return hipErrorInvalidValue;   // gen_walk_masks: 4 / dt = T / 6 for the 1 h day
     const size_t veh = generate_lds_bytes(p.req_enabled != 0), tile = (size_t)round4(kObsEnvs * p.obs_dim) * 4;
     const bool fused = tile <= 32 * 1024;   // up to 60 chargers (config 5's 50: 27.9 KB)
     const dim3 grid((unsigned)((E + kGenBlock - 1) / kGenBlock), (unsigned)(gen_rows(p.n) + (fused ? kObsBlocks : 0))),
