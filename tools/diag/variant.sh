@@ -6,7 +6,8 @@
 #      tools/diag/variant.sh refold -p tools/diag/patches/ref_day2_one_wave.patch
 # A patch under tools/diag/patches/ applies to the source of the commit that added it (later kernel changes
 # can move its context); profiles/r05_ab_*.txt name the builds each A/B compared.
-# STAMPS=1 builds the diagnostic stamps build (SNG_DIAG_STAMPS) of the variant instead.
+# STAMPS=1 builds the diagnostic stamps build (SNG_DIAG_STAMPS) of the variant instead, MEMFLOOR=1 its memory-floor
+# build (SNG_DIAG_MEMFLOOR: trivial charger arithmetic).
 set -euo pipefail
 ROOT=$(cd "$(dirname "$0")/../.." && pwd)
 name=$1; shift
@@ -20,11 +21,12 @@ fi
 if cmp -s "$tmp/csrc/sng_kernels.hip" "$ROOT/smart-nanogrid-gym_amd/csrc/sng_kernels.hip"; then
   echo "variant.sh: the edit changed nothing" >&2; rm -rf "$tmp"; exit 2
 fi
-if [ "${STAMPS:-0}" = 1 ]; then
+if [ "${STAMPS:-0}" = 1 ] || [ "${MEMFLOOR:-0}" = 1 ]; then
+  kind=$([ "${STAMPS:-0}" = 1 ] && echo stamps || echo memfloor)
   cp "$ROOT/tools/diag/sng_kernels_diag.hip" "$tmp/csrc/"
   mkdir -p "$tmp/lib"
-  make -s -C "$ROOT/tools/diag" CSRC="$tmp/csrc" OUT="$tmp/lib" "$tmp/lib/libsng_stamps.so"
-  cp "$tmp/lib/libsng_stamps.so" "$ROOT/smart-nanogrid-gym_amd/lib/libsng_${name}.so"
+  make -s -C "$ROOT/tools/diag" CSRC="$tmp/csrc" OUT="$tmp/lib" "$tmp/lib/libsng_${kind}.so"
+  cp "$tmp/lib/libsng_${kind}.so" "$ROOT/smart-nanogrid-gym_amd/lib/libsng_${name}.so"
 else
   make -s -C "$tmp/csrc" ROOT="$ROOT" OUT="$tmp/lib" "$tmp/lib/libsng.so"
   cp "$tmp/lib/libsng.so" "$ROOT/smart-nanogrid-gym_amd/lib/libsng_${name}.so"

@@ -24,7 +24,8 @@ echo "=== build id $(cat $OUT/build_id.txt)" | tee -a $OUT/session.log
 STEPS="${STEPS:-tests smoke bench prof}"
 for s in $STEPS; do
   case $s in
-    tests) run pytest_gpu 1100 python -u -m pytest tests -m gpu -q -ra --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    tests) if [ -n "${PYTEST_K:-}" ]; then run pytest_gpu 1100 python -u -m pytest tests -m gpu -q -ra --timeout 300 --timeout-method thread -k "$PYTEST_K"
+           else run pytest_gpu 1100 python -u -m pytest tests -m gpu -q -ra --timeout 300 --timeout-method thread ${PYTEST_ARGS:-}; fi ;;
     one)   run pytest_one 600 python -m pytest ${ONE_TESTS:-tests/test_gpu_recorder.py} -m gpu -q ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
