@@ -1026,8 +1026,6 @@ struct WideGroup {
         act_tile.issue(act + e0 * Ad, nw * Ad, vec_io != 0, lane);
         ratio = bld(s.ratio, el8);
         bess_l = bld(p.bess ? s.bess : s.ratio, el8);
-        pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
-        ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
 #pragma unroll
         for (int j = 0; j < 4; ++j) fpv[j] = fpr[j] = 1.0;
         if constexpr (NOISE) profile_factors(p, s, el8, t, fpv, fpr);   // the day's profile factors of t..t+3
@@ -1059,6 +1057,14 @@ struct WideGroup {
             }
             if (REQ) req[REQ ? j : 0] = bld(s.req + plane, v8, r8);
         }
+        // the t = 0 penalty and the day return are read only by the env tail: issued behind every charger's
+        // loads, so the waits before the chargers (the header's PV ratio, the BESS step's SoC) do not count them
+        // (round 6, A/B in the day graph: 6.36 -> 6.25-6.29 us per step, profiles/r06_ab_step_tail_order.txt).
+        // Stores issued earlier or in bursts measured slower there: the observation tile stored before the env
+        // tail +0.33 us, its copy-out unrolled (every LDS read, then every 16 B store) +0.6 us, the SoC pairs
+        // stored after the charger loop +0.3 us -- paced stores leave the other wavefronts' loads alone.
+        pen0_l = bld(t == 0 ? s.pen0 : s.ratio, el8);
+        ret_l = bld(info.episode_return ? info.episode_return : s.ratio, el8);
     }
     // Requested_SOC[c, t-1] of charger j of the lane; without the stream 1.0, or the cleared 0.0 of a replayed day
     __device__ __forceinline__ double req_of(int j, const Params &p) const {
