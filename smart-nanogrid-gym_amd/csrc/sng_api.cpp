@@ -1279,12 +1279,27 @@ int sng_reset_from_scenario(SngEnv *env, const SngScenario *sc, float *obs, void
     return SNG_OK;
 }
 
+// The handle's device for the length of a call, the caller's current device restored after it (sng_step and
+// sng_step_host are called per step without a device guard of the caller's own).
+struct DeviceScope {
+    int prev = -1, dev;
+    hipError_t err = hipSuccess;
+    explicit DeviceScope(int d) : dev(d) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != d) err = hipSetDevice(d);
+    }
+    ~DeviceScope() {
+        if (prev >= 0 && prev != dev) (void)hipSetDevice(prev);
+    }
+};
+
 int sng_step(SngEnv *env, const float *actions, float *obs, double *reward, uint8_t *done, const SngInfo *info,
              void *stream) {
     if (!env || !actions || !obs || !reward || !done) return fail(env, SNG_ERR_INVALID_ARGUMENT, "null argument");
     if (env->t < 0) return fail(env, SNG_ERR_STATE, "step() before reset()");
     if (env->t >= env->p.T) return fail(env, SNG_ERR_STATE, "the day is over: call reset()");
-    HIP_TRY(env, hipSetDevice(env->device));
+    DeviceScope dev(env->device);
+    HIP_TRY(env, dev.err);
     const int vec = (aligned16(actions) && aligned16(obs)) ? 1 : 0;
     HIP_TRY(env, launch_step(env->p, env->ds, info_ptrs(info), env->host_tab, actions, obs, reward, done, env->E, env->t, vec,
                              as_stream(stream)));
@@ -1301,7 +1316,8 @@ int sng_step_host(SngEnv *env, const float *actions, float *obs, double *reward,
     if (env->t >= env->p.T) return fail(env, SNG_ERR_STATE, "the day is over: call reset()");
     if (info && info->flags)
         return fail(env, SNG_ERR_INVALID_ARGUMENT, "sng_step_host returns the step's flags itself: SngInfo.flags must be null");
-    HIP_TRY(env, hipSetDevice(env->device));
+    DeviceScope dev(env->device);
+    HIP_TRY(env, dev.err);
     hipStream_t st = as_stream(stream);
     const size_t E = (size_t)env->E, A = (size_t)env->p.act_dim, O = (size_t)env->p.obs_dim;
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };

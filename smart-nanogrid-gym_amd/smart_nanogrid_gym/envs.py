@@ -12,7 +12,7 @@ import torch
 
 from ._native import check, lib
 from .recorder import DayRecorder
-from .vec_env import SmartNanogridVecEnv
+from .vec_env import SmartNanogridVecEnv, _raw_stream
 
 try:  # subclass gym(nasium).Env when available so wrappers / checkers accept it
     import gymnasium as _gym   # pragma: no cover - not in the image
@@ -24,15 +24,6 @@ except Exception:
 
 _Base = _gym.Env if _gym is not None else object
 
-_get_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
-
-
-def _raw_stream(index):
-    """torch's current stream on device `index` as a hipStream_t: the raw handle when torch exposes it (~0.3 us),
-    else through torch.cuda.current_stream."""
-    if _get_raw_stream is not None:
-        return _get_raw_stream(index)
-    return torch.cuda.current_stream(index).cuda_stream
 
 
 class SmartNanogridEnv(_Base):

@@ -159,8 +159,19 @@ def _host_copy(pinned):
     return out
 
 
+_get_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None) if torch is not None else None
+
+
+def _raw_stream(index):
+    """torch's current stream on device `index` as a hipStream_t (int): the raw handle when torch exposes it
+    (~0.3 us; torch.cuda.current_stream builds a Stream object, ~2 us), else through current_stream."""
+    if _get_raw_stream is not None:
+        return _get_raw_stream(index)
+    return torch.cuda.current_stream(index).cuda_stream
+
+
 def _stream_handle(device):
-    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    return ctypes.c_void_p(_raw_stream(device.index or 0))
 
 
 class SmartNanogridVecEnv(_VecEnvBase):
@@ -237,6 +248,12 @@ class SmartNanogridVecEnv(_VecEnvBase):
             self._enable_info()
         # pinned host mirror of the actions for the numpy (SB3) path
         self._act_h = torch.zeros((E, self.act_dim), dtype=torch.float32, pin_memory=True)
+        # step_tensors' fixed arguments (the output buffers and SngInfo never move)
+        self._dev_index = self.device.index or 0
+        self._act_shape = torch.Size((E, self.act_dim))
+        self._sng_step = lib().sng_step
+        self._step_args = (ctypes.c_void_p(self.obs_d.data_ptr()), ctypes.c_void_p(self.reward_d.data_ptr()),
+                           ctypes.c_void_p(self.done_d.data_ptr()), ctypes.byref(self._info))
         self._prof = None
         self._pending = None
         self._warned_breakpoint = False
@@ -335,15 +352,18 @@ class SmartNanogridVecEnv(_VecEnvBase):
 
     def step_tensors(self, actions):
         """One step for every env from device actions [E, act_dim] float32.
-        Returns (obs [E, obs_dim] f32, reward [E] f64, done [E] u8) device tensors, no auto-reset."""
-        if actions.dtype != torch.float32 or actions.device != self.device or not actions.is_contiguous():
+        Returns (obs [E, obs_dim] f32, reward [E] f64, done [E] u8) device tensors, no auto-reset.
+        The call only enqueues the step on torch's current stream of the env's device (sng_step selects the
+        device itself); its fixed arguments are built once, so the host keeps ahead of a ~6 us step
+        (profiles/r06_reset_bench.log: an eager day of step_tensors calls)."""
+        if (actions.dtype != torch.float32 or actions.get_device() != self._dev_index
+                or not actions.is_contiguous()):
             actions = actions.to(device=self.device, dtype=torch.float32).contiguous()
-        if tuple(actions.shape) != (self.num_envs, self.act_dim):
+        if actions.shape != self._act_shape:
             raise ValueError(f"actions must have shape {(self.num_envs, self.act_dim)}")
-        with torch.cuda.device(self.device):
-            check(lib().sng_step(self._h, ctypes.c_void_p(actions.data_ptr()), ctypes.c_void_p(self.obs_d.data_ptr()),
-                                 ctypes.c_void_p(self.reward_d.data_ptr()), ctypes.c_void_p(self.done_d.data_ptr()),
-                                 ctypes.byref(self._info), _stream_handle(self.device)), self._h)
+        rc = self._sng_step(self._h, actions.data_ptr(), *self._step_args, _raw_stream(self._dev_index))
+        if rc:
+            check(rc, self._h)
         for r in self._recorders:
             r.step_done(actions)
         return self.obs_d, self.reward_d, self.done_d
