@@ -60,6 +60,7 @@ for s in $STEPS; do
             run single_env_torch 300 python tools/single_env_bench.py --path torch
             run single_env_device 300 python tools/single_env_bench.py --rng device ;;
     iolat) run io_latency 120 tools/io_latency ;;
+    overlap) run overlap_probe 300 python tools/overlap_probe.py ;;
     genab) for l in ${AB_LIBS:?}; do SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "genab_$l" 300 python tools/diag/gen_ab_check.py; done
            set -- ${AB_LIBS}; if diff <(grep '^E=' $OUT/genab_$1.log) <(grep '^E=' $OUT/genab_$2.log) > $OUT/genab_diff.txt; then echo "genab: identical" | tee -a $OUT/session.log; else echo "genab: DIFFER" | tee -a $OUT/session.log; fi ;;
     sqsalu) for l in ${SQ_LIBS:-libsng}; do SNG_LIBRARY=smart-nanogrid-gym_amd/lib/$l.so run "sqsalu_$l" 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU -d $OUT/sqsalu_$l -o run --output-format csv -- python bench.py --no-cpu-baseline --steps 3 --warmup 1; done ;;
