@@ -403,6 +403,60 @@ def test_single_env_host_step_equals_device_buffer_step(n, v2x, rng):
         e.close()
 
 
+@pytest.mark.parametrize("E,N", [(100, 10), (333, 4), (70, 50)])
+def test_step_host_batches_equal_step(E, N):
+    """sng_step_host over a batch (several wavefronts, a ragged last one) writes the same observations, rewards and
+    done flags into host memory as sng_step does into device buffers, and reports each env's step flags."""
+    from smart_nanogrid_gym import _native
+    kw = dict(number_of_chargers=N, time_interval="1h", charging_mode="bounded",
+              vehicle_uncharged_penalty_mode="dense")
+    a_env = SmartNanogridVecEnv(E, seed=8, rng="reference", **kw)
+    b_env = SmartNanogridVecEnv(E, seed=8, rng="reference", **kw)
+    a_env.reset_tensors()
+    b_env.reset_tensors()
+    rng = np.random.default_rng(E)
+    lo, hi = a_env.action_space.low, a_env.action_space.high
+    obs = np.zeros((E, a_env.obs_dim), np.float32)
+    rew = np.zeros(E)
+    done = np.zeros(E, np.uint8)
+    flags = np.zeros(E, np.uint32)
+    P = lambda x: ctypes.c_void_p(x.ctypes.data)   # noqa: E731
+    for t in range(a_env.timesteps):
+        act = (lo + (hi - lo) * rng.random((E, lo.size))).astype(np.float32)
+        act[rng.random(act.shape) < 0.2] = 0
+        o, r, d = a_env.step_tensors(torch.from_numpy(act).to(a_env.device))
+        _native.check(_native.lib().sng_step_host(b_env._h, P(act), P(obs), P(rew), P(done), P(flags),
+                                                  ctypes.byref(b_env._info), ctypes.c_void_p(0)), b_env._h)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(obs, o.cpu().numpy())
+        np.testing.assert_array_equal(rew, r.cpu().numpy())
+        np.testing.assert_array_equal(done, d.cpu().numpy())
+        assert not flags.any()
+    a_env.close()
+    b_env.close()
+
+
+def test_step_tensors_converts_its_input():
+    """step_tensors takes host, float64 and non-contiguous actions (converted to a contiguous float32 device tensor)
+    and refuses a wrong shape; every form steps to the same day."""
+    kw = dict(number_of_chargers=4, time_interval="1h", charging_mode="bounded", vehicle_uncharged_penalty_mode="sparse")
+    envs = [SmartNanogridVecEnv(64, seed=2, rng="device", **kw) for _ in range(3)]
+    for v in envs:
+        v.reset_tensors()
+    g = torch.Generator().manual_seed(0)
+    for t in range(24):
+        a = torch.rand((5, 64), generator=g).t()                 # non-contiguous, host, float32
+        outs = [envs[0].step_tensors(a.contiguous().to(envs[0].device)),
+                envs[1].step_tensors(a),
+                envs[2].step_tensors(a.double())]
+        for o in outs[1:]:
+            assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
+    with pytest.raises(ValueError, match="shape"):
+        envs[0].step_tensors(torch.zeros((64, 4), device=envs[0].device))
+    for v in envs:
+        v.close()
+
+
 def test_single_env_host_step_raises_reference_errors():
     """The host path's per-step flags raise the reference's ValueError at the step that hit it (charging_mode=''
     leaves the positive-action branch unimplemented, charger.py:88) and refuse a wrong action size."""
