@@ -108,8 +108,8 @@ class StepInfos(collections.abc.Sequence):
                 out[i]["v2x_breakpoint"] = True
             for i, d in self._made.items():
                 out[i] = d
-            self._all = out
-            self._made = dict(enumerate(out))
+            self._all = out   # from now on every access reads this list
+            self._made = None
         return self._all
 
     def __getitem__(self, i):
