@@ -18,7 +18,7 @@ if [ "$1" = "-p" ]; then
 else
   sed -i "$1" "$tmp/csrc/sng_kernels.hip"
 fi
-if cmp -s "$tmp/csrc/sng_kernels.hip" "$ROOT/smart-nanogrid-gym_amd/csrc/sng_kernels.hip"; then
+if diff -rq "$tmp/csrc" "$ROOT/smart-nanogrid-gym_amd/csrc" > /dev/null; then
   echo "variant.sh: the edit changed nothing" >&2; rm -rf "$tmp"; exit 2
 fi
 if [ "${STAMPS:-0}" = 1 ] || [ "${MEMFLOOR:-0}" = 1 ]; then
