@@ -1,3 +1,7 @@
+#!/bin/bash
+# A generator rewrite against the build before it (profiles/r06_ab_generator_obs_rows.txt): copy the old library to
+# lib/libsng_base.so, build the new one as lib/libsng.so (e.g. with tools/diag/patches/generator_obs_in_timeline.patch
+# applied), then: every device day must hash the same (tools/diag/gen_ab_check.py), and the bench A/B follows.
 set -uo pipefail
 L=smart-nanogrid-gym_amd/lib
 SNG_LIBRARY=$L/libsng_base.so timeout -k 10 300 python tools/diag/gen_ab_check.py > gpurun_out/genobs_a.txt 2>&1 || { tail -5 gpurun_out/genobs_a.txt; exit 1; }
