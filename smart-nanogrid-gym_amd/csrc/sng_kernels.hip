@@ -1973,8 +1973,8 @@ __device__ __forceinline__ void observe_day0(const Params &p, const DeviceState 
 //     then arrival SoC, capacity and departure -- a few draws per vehicle instead of one per free
 //     step, without the per-step divergent arrival branch;
 //  2. the dense timeline, step by step, from the vehicle list kept in LDS.
-// Grid (E / 256, 4 + N): blocks y < 4 the t = 0 observation (observe_day0), blocks y >= 4 charger
-// y - 4's timeline.  The day counter is read here and advanced by the day's first step
+// Grid (E / 256, rows + 4): blocks y < gen_rows(N) the timeline of charger quad y / 4, the last 4 rows the
+// t = 0 observation (observe_day0).  The day counter is read here and advanced by the day's first step
 // (step_kernel, t = 0), so no block of this grid waits on another.
 // The timeline records leave as streaming (nontemporal) stores: reset 24.5-24.7 -> 22.5-22.7 us per day
 // at 65,536 x 10 (A/B, one box), the steps' code and state staying in L2.  Diagnostic builds
@@ -2006,16 +2006,16 @@ __global__ __launch_bounds__(kGenBlock) void generate_kernel(Params p, DeviceSta
     uint32_t *s_car = s_veh + kDaySlots * kGenBlock;                           // [V][BLOCK] arrival SoC carry bits
     double *s_req = reinterpret_cast<double *>(s_car + kDaySlots * kGenBlock);     // [V][BLOCK] (REQ only)
     const int tid = threadIdx.x;
-    // grid rows: the t = 0 observation blocks first (gridDim.y - gen_rows(N) of them: dispatched first,
-    // their dependent table and BESS loads do not trail the timeline blocks), then the timeline: row u
-    // of charger quad u / 4 and 64 envs [256 x + 64 (u mod 4), +64), thread = (env tid / 4, charger tid mod 4
-    // of the quad), so a wavefront's record stores are 16 envs x the quad's records, contiguous in the
-    // quad layout (sng_layout.h rec_index)
-    const int obs_rows = (int)gridDim.y - gen_rows(p.n);
-    const int u = (int)blockIdx.y - obs_rows;
+    // grid rows: the timeline first, row u of charger quad u / 4 and 64 envs [256 x + 64 (u mod 4), +64), thread =
+    // (env tid / 4, charger tid mod 4 of the quad), so a wavefront's record stores are 16 envs x the quad's
+    // records, contiguous in the quad layout (sng_layout.h rec_index); then the t = 0 observation blocks
+    // (gridDim.y - gen_rows(N) of them).  Dispatched last, they fill the CUs behind the timeline's VALU-bound
+    // waves instead of delaying them: reset 16.0-16.3 -> 15.5-15.6 us (A/B three times on one box, same days,
+    // profiles/r06_ab_generator_obs_order.txt; round 3's kernel had measured the opposite order 0.6 % better)
+    const int u = (int)blockIdx.y;
     const uint64_t day = *s.episode;
-    if (u < 0) {
-        observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds, (int)blockIdx.y);
+    if (u >= gen_rows(p.n)) {
+        observe_day0(p, s, seed, E, i4, i10, i1, day, obs, ep_return, vec_io, lds, u - gen_rows(p.n));
         return;
     }
     const int full = 4 * (p.n / 4);                              // timeline rows of the full quads
