@@ -107,12 +107,14 @@ def _xch_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_overlapped_day_return_exchange():
-    """DayReturnExchange: double-buffered asynchronous all-gather of [days, E] day returns."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_overlapped_day_return_exchange(world):
+    """DayReturnExchange: double-buffered asynchronous all-gather of [days, E] day returns, at the world sizes the
+    driver's scaling run uses (8 ranks as bench.py's 8 GPUs; gloo on the CPU here)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_xch_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_xch_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     results = q.get(timeout=240)
@@ -122,7 +124,7 @@ def test_gloo_world2_overlapped_day_return_exchange():
     assert len(results) == 4
     base = np.arange(15, dtype=np.float64).reshape(3, 5)
     for rep, got in enumerate(results):
-        want = np.concatenate([base + 1000 * r + 100 * rep for r in range(2)], axis=1)
+        want = np.concatenate([base + 1000 * r + 100 * rep for r in range(world)], axis=1)
         np.testing.assert_array_equal(got, want)
 
 
